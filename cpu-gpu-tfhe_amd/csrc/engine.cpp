@@ -1,0 +1,497 @@
+// engine.cpp — device contexts, key upload, scratch and the Tier-2 (batched) C ABI.
+//
+// Replaces the reference GPU host glue: key upload (gpuParallel/main.cu:165-213, 236-254,
+// 364-407), the per-gate chunking / temp allocation of bootsAND_fullGPU_n_Bit
+// (boot-gates.cu:2845-2915) and bootstrapAndKeySwitch_n_Bit (:2481-2629).  Differences
+// by design: keys are uploaded once per (cloud key, GPU) in the coefficient domain and
+// converted on the device; ciphertext b-halves stay on the device; no per-call FFT plans,
+// no host round trips inside a batch; work is enqueued on a caller-chosen stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "engine.h"
+#include "ntt_tables.h"
+#include "../../include/tfhe_amd.h"
+
+namespace tfhe_amd {
+
+// ------------------------------------------------------------------ tables
+
+uint32_t host_powmod(uint32_t b, uint64_t e, uint32_t q) {
+    uint64_t r = 1, x = b % q;
+    while (e) {
+        if (e & 1) r = r * x % q;
+        x = x * x % q;
+        e >>= 1;
+    }
+    return (uint32_t)r;
+}
+
+static unsigned brv(unsigned x, int bits) {
+    unsigned r = 0;
+    for (int i = 0; i < bits; i++) { r = (r << 1) | (x & 1); x >>= 1; }
+    return r;
+}
+static uint32_t shoup(uint32_t w, uint32_t q) { return (uint32_t)(((uint64_t)w << 32) / q); }
+
+void build_ntt_tables(NttTables *t) {
+    for (int s = 0; s < 2; s++) {
+        const uint32_t q = kQ[s];
+        uint32_t psi = 0;
+        for (uint32_t g = 2; g < 1000 && !psi; g++) {
+            const uint32_t c = host_powmod(g, (q - 1) / k2N, q);
+            if (host_powmod(c, kN, q) == q - 1) psi = c;   // primitive 2N-th root
+        }
+        const uint32_t ipsi = host_powmod(psi, q - 2, q);
+        for (int k = 0; k < kN; k++) {
+            t->psi[s][k] = host_powmod(psi, brv(k, kLogN), q);
+            t->psip[s][k] = shoup(t->psi[s][k], q);
+            t->ipsi[s][k] = host_powmod(ipsi, brv(k, kLogN), q);
+            t->ipsip[s][k] = shoup(t->ipsi[s][k], q);
+        }
+        t->ninv[s] = host_powmod(kN, q - 2, q);
+        // -q^-1 mod 2^32 by Newton iteration
+        uint32_t inv = q;
+        for (int it = 0; it < 5; it++) inv *= 2u - q * inv;
+        t->qinv_neg[s] = 0u - inv;
+        const uint32_t r_mod_q = (uint32_t)((1ull << 32) % q);
+        t->bk_scale[s] = (uint32_t)((uint64_t)t->ninv[s] * r_mod_q % q);
+        t->bk_scalep[s] = shoup(t->bk_scale[s], q);
+    }
+    t->crt_h = host_powmod(kQ[0] % kQ[1], kQ[1] - 2, kQ[1]);
+    t->crt_hp = shoup(t->crt_h, kQ[1]);
+}
+
+}  // namespace tfhe_amd
+
+using namespace tfhe_amd;
+
+// ------------------------------------------------------------------ context
+
+struct TfheAmdContext {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DeviceKey key;
+    // scratch (device)
+    int cap = 0;
+    int32_t *u_a = nullptr;   // [2 cap][kN]   extracted samples (2 halves for MUX)
+    int32_t *u_b = nullptr;   // [2 cap]
+    int32_t *io = nullptr;    // host-API staging: inputs 3 x (cap x 501) + outputs cap x 501
+    // pinned host staging for the host API
+    int32_t *h_io = nullptr;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> br_ev, ks_ev;
+    double br_ms = 0, ks_ms = 0;
+    int br_n = 0, ks_n = 0;
+    std::mutex mu;
+    bool shared_key = false;   // lane: the key belongs to another context
+};
+
+#define HIPCHK(x)                                                                 \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            fprintf(stderr, "tfhe_amd: %s failed: %s (%s:%d)\n", #x,              \
+                    hipGetErrorString(e_), __FILE__, __LINE__);                   \
+            return TFHE_AMD_E_HIP;                                                \
+        }                                                                         \
+    } while (0)
+
+static int free_key(DeviceKey &k) {
+    if (k.device >= 0) (void)hipSetDevice(k.device);
+    if (k.bk_ntt) (void)hipFree(k.bk_ntt);
+    if (k.ksk) (void)hipFree(k.ksk);
+    if (k.tables) (void)hipFree(k.tables);
+    k = DeviceKey();
+    return 0;
+}
+
+static int free_scratch(TfheAmdContext *c) {
+    if (c->u_a) (void)hipFree(c->u_a);
+    if (c->u_b) (void)hipFree(c->u_b);
+    if (c->io) (void)hipFree(c->io);
+    if (c->h_io) (void)hipHostFree(c->h_io);
+    c->u_a = c->u_b = c->io = c->h_io = nullptr;
+    c->cap = 0;
+    return 0;
+}
+
+static size_t io_words(int cap) { return (size_t)4 * cap * (kn + 1); }
+
+int tfhe_amd_reserve(TfheAmdContext *c, int B) {
+    if (!c || B < 0) return TFHE_AMD_E_ARG;
+    if (B <= c->cap) return TFHE_AMD_OK;
+    int cap = c->cap ? c->cap : 64;
+    while (cap < B) cap *= 2;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    free_scratch(c);
+    HIPCHK(hipMalloc(&c->u_a, sizeof(int32_t) * 2 * (size_t)cap * kN));
+    HIPCHK(hipMalloc(&c->u_b, sizeof(int32_t) * 2 * (size_t)cap));
+    HIPCHK(hipMalloc(&c->io, sizeof(int32_t) * io_words(cap)));
+    HIPCHK(hipHostMalloc(&c->h_io, sizeof(int32_t) * io_words(cap), hipHostMallocDefault));
+    c->cap = cap;
+    return TFHE_AMD_OK;
+}
+
+// Upload: bk [kn][4][2][kN] (nullable: KS-only context), ksk [kN][8][4][kn+1]
+static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk, int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return TFHE_AMD_E_NODEVICE;
+    if (device < 0 || device >= ndev) return TFHE_AMD_E_ARG;
+    c->device = device;
+    c->key.device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+
+    NttTables *ht = new NttTables;
+    build_ntt_tables(ht);
+    HIPCHK(hipMalloc(&c->key.tables, sizeof(NttTables)));
+    HIPCHK(hipMemcpy(c->key.tables, ht, sizeof(NttTables), hipMemcpyHostToDevice));
+    delete ht;
+
+    if (bk) {
+        const size_t coef_words = (size_t)kn * kKpl * 2 * kN;
+        int32_t *d_coef = nullptr;
+        HIPCHK(hipMalloc(&d_coef, sizeof(int32_t) * coef_words));
+        HIPCHK(hipMemcpy(d_coef, bk, sizeof(int32_t) * coef_words, hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&c->key.bk_ntt, sizeof(uint32_t) * 2 * coef_words));
+        HIPCHK(launch_bk_to_ntt(d_coef, c->key.bk_ntt, c->key.tables, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipFree(d_coef));
+        c->key.has_bk = true;
+    }
+    if (ksk) {
+        // drop the zero digit h = 0 (lwe-keyswitch-functions.cu:919), pad rows to 512 words
+        const size_t rows = (size_t)kN * kKsT * 3;
+        std::vector<int32_t> packed(rows * kKsRow, 0);
+        for (int i = 0; i < kN; i++)
+            for (int j = 0; j < kKsT; j++)
+                for (int h = 1; h < kKsBase; h++) {
+                    const int32_t *src = ksk + (((size_t)i * kKsT + j) * kKsBase + h) * (kn + 1);
+                    int32_t *dst = packed.data() + (((size_t)i * kKsT + j) * 3 + (h - 1)) * kKsRow;
+                    memcpy(dst, src, sizeof(int32_t) * (kn + 1));
+                }
+        HIPCHK(hipMalloc(&c->key.ksk, sizeof(int32_t) * packed.size()));
+        HIPCHK(hipMemcpy(c->key.ksk, packed.data(), sizeof(int32_t) * packed.size(), hipMemcpyHostToDevice));
+    }
+    return tfhe_amd_reserve(c, 64);
+}
+
+extern "C" int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk, int device,
+                                           TfheAmdContext **out) {
+    if (!out || (!bk && !ksk)) return TFHE_AMD_E_ARG;
+    TfheAmdContext *c = new TfheAmdContext();
+    int rc = context_init(c, bk, ksk, device);
+    if (rc != TFHE_AMD_OK) {
+        tfhe_amd_context_destroy(c);
+        *out = nullptr;
+        return rc;
+    }
+    *out = c;
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
+    if (!c) return TFHE_AMD_OK;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    for (auto &p : c->ks_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    free_scratch(c);
+    if (!c->shared_key) free_key(c->key);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_context_device(const TfheAmdContext *c) { return c ? c->device : -1; }
+extern "C" void *tfhe_amd_context_stream(TfheAmdContext *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" int tfhe_amd_sync(TfheAmdContext *c) {
+    if (!c) return TFHE_AMD_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TFHE_AMD_OK;
+}
+
+// ------------------------------------------------------------------ profiling
+
+static void prof_collect(TfheAmdContext *c) {
+    for (auto *vec : {&c->br_ev, &c->ks_ev}) {
+        for (auto &p : *vec) {
+            float ms = 0;
+            (void)hipEventSynchronize(p.second);
+            (void)hipEventElapsedTime(&ms, p.first, p.second);
+            if (vec == &c->br_ev) { c->br_ms += ms; c->br_n++; }
+            else { c->ks_ms += ms; c->ks_n++; }
+            (void)hipEventDestroy(p.first);
+            (void)hipEventDestroy(p.second);
+        }
+        vec->clear();
+    }
+}
+
+extern "C" int tfhe_amd_profile_enable(TfheAmdContext *c, int enable) {
+    if (!c) return TFHE_AMD_E_ARG;
+    (void)hipSetDevice(c->device);
+    prof_collect(c);
+    c->prof = enable != 0;
+    c->br_ms = c->ks_ms = 0;
+    c->br_n = c->ks_n = 0;
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_profile_read(TfheAmdContext *c, double *br_ms, int *br_n, double *ks_ms, int *ks_n) {
+    if (!c) return TFHE_AMD_E_ARG;
+    (void)hipSetDevice(c->device);
+    prof_collect(c);
+    if (br_ms) *br_ms = c->br_ms;
+    if (br_n) *br_n = c->br_n;
+    if (ks_ms) *ks_ms = c->ks_ms;
+    if (ks_n) *ks_n = c->ks_n;
+    return TFHE_AMD_OK;
+}
+
+struct ProfScope {
+    TfheAmdContext *c;
+    hipStream_t s;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> *vec;
+    hipEvent_t a = nullptr;
+    ProfScope(TfheAmdContext *c_, hipStream_t s_, bool br) : c(c_), s(s_), vec(br ? &c_->br_ev : &c_->ks_ev) {
+        if (c->prof) {
+            (void)hipEventCreate(&a);
+            (void)hipEventRecord(a, s);
+        }
+    }
+    ~ProfScope() {
+        if (c->prof && a) {
+            hipEvent_t b;
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(b, s);
+            vec->push_back({a, b});
+        }
+    }
+};
+
+// ------------------------------------------------------------------ batches
+
+static bool gate_spec(int gate, int32_t *c, int32_t *sa, int32_t *sb) {
+    // constants of boot-gates.cu:98-397 (modSwitchToTorus32(+-1, 8) = +-2^29, (+-1, 4) = +-2^30)
+    const int32_t e8 = 1 << 29, e4 = 1 << 30;
+    switch (gate) {
+    case TFHE_GATE_NAND:  *c = e8;  *sa = -1; *sb = -1; return true;
+    case TFHE_GATE_OR:    *c = e8;  *sa = 1;  *sb = 1;  return true;
+    case TFHE_GATE_AND:   *c = -e8; *sa = 1;  *sb = 1;  return true;
+    case TFHE_GATE_XOR:   *c = e4;  *sa = 2;  *sb = 2;  return true;
+    case TFHE_GATE_XNOR:  *c = -e4; *sa = -2; *sb = -2; return true;
+    case TFHE_GATE_NOR:   *c = -e8; *sa = -1; *sb = -1; return true;
+    case TFHE_GATE_ANDNY: *c = -e8; *sa = -1; *sb = 1;  return true;
+    case TFHE_GATE_ANDYN: *c = -e8; *sa = 1;  *sb = -1; return true;
+    case TFHE_GATE_ORNY:  *c = e8;  *sa = -1; *sb = 1;  return true;
+    case TFHE_GATE_ORYN:  *c = e8;  *sa = 1;  *sb = -1; return true;
+    default: return false;
+    }
+}
+
+static const int32_t kMu = 1 << 29;   // modSwitchToTorus32(1, 8)
+
+extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
+                                       const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
+                                       const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b,
+                                       void *stream) {
+    if (!c || B < 0 || !c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = tfhe_amd_reserve(c, B);
+    if (rc) return rc;
+    if (gate == TFHE_GATE_MUX) {
+        if (!cc_a || !cc_b) return TFHE_AMD_E_ARG;
+        // boot-gates.cu:407-448: u1 = woKS(-1/8 + a + b), u2 = woKS(-1/8 - a + c),
+        // result = KS((0, 1/8) + u1 + u2)
+        BrInput in[2] = {{ca_a, ca_b, cb_a, cb_b, -kMu, 1, 1}, {ca_a, ca_b, cc_a, cc_b, -kMu, -1, 1}};
+        {
+            ProfScope ps(c, s, true);
+            HIPCHK(launch_blind_rotate(c->key, B, 2, in, kMu, c->u_a, c->u_b, s));
+        }
+        ProfScope ps(c, s, false);
+        HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, c->u_a + (size_t)B * kN, c->u_b + B, kMu,
+                                res_a, res_b, s));
+        return TFHE_AMD_OK;
+    }
+    BrInput in;
+    if (!gate_spec(gate, &in.c, &in.sa, &in.sb)) return TFHE_AMD_E_ARG;
+    in.x_a = ca_a; in.x_b = ca_b; in.y_a = cb_a; in.y_b = cb_b;
+    {
+        ProfScope ps(c, s, true);
+        HIPCHK(launch_blind_rotate(c->key, B, 1, &in, kMu, c->u_a, c->u_b, s));
+    }
+    ProfScope ps(c, s, false);
+    HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32_t mu, const int32_t *x_a,
+                                                 const int32_t *x_b, int32_t *u_a, int32_t *u_b, void *stream) {
+    if (!c || B < 0 || !c->key.has_bk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!x_a || !x_b || !u_a || !u_b) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
+    ProfScope ps(c, s, true);
+    HIPCHK(launch_blind_rotate(c->key, B, 1, &in, mu, u_a, u_b, s));
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu, const int32_t *x_a,
+                                            const int32_t *x_b, int32_t *res_a, int32_t *res_b, void *stream) {
+    if (!c || B < 0 || !c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!x_a || !x_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = tfhe_amd_reserve(c, B);
+    if (rc) return rc;
+    BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
+    {
+        ProfScope ps(c, s, true);
+        HIPCHK(launch_blind_rotate(c->key, B, 1, &in, mu, c->u_a, c->u_b, s));
+    }
+    ProfScope ps(c, s, false);
+    HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_keyswitch_batch_dev(TfheAmdContext *c, int B, const int32_t *u_a, const int32_t *u_b,
+                                            int32_t *res_a, int32_t *res_b, void *stream) {
+    if (!c || B < 0 || !c->key.ksk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!u_a || !u_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    ProfScope ps(c, s, false);
+    HIPCHK(launch_keyswitch(c->key, B, u_a, u_b, nullptr, nullptr, 0, res_a, res_b, s));
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, int32_t *acc, const int32_t *bara,
+                                         void *stream) {
+    if (!c || B < 0 || iters < 0 || iters > kn || !c->key.has_bk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!acc || (iters > 0 && !bara)) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    ProfScope ps(c, s, true);
+    HIPCHK(launch_blind_rotate_debug(c->key, B, iters, acc, bara, s));
+    return TFHE_AMD_OK;
+}
+
+// host batch: stage inputs into pinned memory, one H2D, the device batch, one D2H.
+extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
+                                        const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
+                                        const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b) {
+    if (!c || B < 0) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
+    const bool mux = gate == TFHE_GATE_MUX;
+    if (mux && (!cc_a || !cc_b)) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = tfhe_amd_reserve(c, B);
+    if (rc) return rc;
+    const size_t A = (size_t)B * kn;
+    // staging layout: [ca_a | cb_a | cc_a | res_a] then [ca_b | cb_b | cc_b | res_b]
+    int32_t *h = c->h_io;
+    int32_t *d = c->io;
+    const int nin = mux ? 3 : 2;
+    memcpy(h, ca_a, A * 4);
+    memcpy(h + A, cb_a, A * 4);
+    if (mux) memcpy(h + 2 * A, cc_a, A * 4);
+    int32_t *hb = h + 4 * A;
+    memcpy(hb, ca_b, B * 4);
+    memcpy(hb + B, cb_b, B * 4);
+    if (mux) memcpy(hb + 2 * B, cc_b, B * 4);
+    HIPCHK(hipMemcpyAsync(d, h, nin * A * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d + 4 * A, hb, (size_t)nin * B * 4, hipMemcpyHostToDevice, c->stream));
+    int32_t *db = d + 4 * A;
+    rc = tfhe_amd_gate_batch_dev(c, gate, B, d + 3 * A, db + 3 * B, d, db, d + A, db + B,
+                                 mux ? d + 2 * A : nullptr, mux ? db + 2 * B : nullptr, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h + 3 * A, d + 3 * A, A * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(hb + 3 * B, db + 3 * B, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(res_a, h + 3 * A, A * 4);
+    memcpy(res_b, hb + 3 * B, (size_t)B * 4);
+    return TFHE_AMD_OK;
+}
+
+// woKS / bootstrap / KS host versions: same staging scheme (in-place safe)
+enum { OP_WOKS, OP_BOOT, OP_KS };
+static int single_input_host(TfheAmdContext *c, int op, int B, int32_t mu, const int32_t *in_a,
+                             const int32_t *in_b, int32_t *out_a, int32_t *out_b) {
+    if (!c || B < 0) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!in_a || !in_b || !out_a || !out_b) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = tfhe_amd_reserve(c, B);
+    if (rc) return rc;
+    const int din = op == OP_KS ? kN : kn, dout = op == OP_WOKS ? kN : kn;
+    const size_t Ai = (size_t)B * din, Ao = (size_t)B * dout;
+    int32_t *h = c->h_io, *d = c->io;
+    // [in_a | in_b | out_a | out_b]  (<= B * (1025 + 1025) words <= 4 * cap * 501)
+    memcpy(h, in_a, Ai * 4);
+    memcpy(h + Ai, in_b, (size_t)B * 4);
+    HIPCHK(hipMemcpyAsync(d, h, (Ai + B) * 4, hipMemcpyHostToDevice, c->stream));
+    int32_t *oa = d + Ai + B, *ob = oa + Ao;
+    if (op == OP_WOKS) rc = tfhe_amd_bootstrap_woks_batch_dev(c, B, mu, d, d + Ai, oa, ob, c->stream);
+    else if (op == OP_BOOT) rc = tfhe_amd_bootstrap_batch_dev(c, B, mu, d, d + Ai, oa, ob, c->stream);
+    else rc = tfhe_amd_keyswitch_batch_dev(c, B, d, d + Ai, oa, ob, c->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h + Ai + B, oa, (Ao + B) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(out_a, h + Ai + B, Ao * 4);
+    memcpy(out_b, h + Ai + B + Ao, (size_t)B * 4);
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_bootstrap_woks_batch_host(TfheAmdContext *c, int B, int32_t mu, const int32_t *x_a,
+                                                  const int32_t *x_b, int32_t *u_a, int32_t *u_b) {
+    return single_input_host(c, OP_WOKS, B, mu, x_a, x_b, u_a, u_b);
+}
+extern "C" int tfhe_amd_bootstrap_batch_host(TfheAmdContext *c, int B, int32_t mu, const int32_t *x_a,
+                                             const int32_t *x_b, int32_t *res_a, int32_t *res_b) {
+    return single_input_host(c, OP_BOOT, B, mu, x_a, x_b, res_a, res_b);
+}
+extern "C" int tfhe_amd_keyswitch_batch_host(TfheAmdContext *c, int B, const int32_t *u_a, const int32_t *u_b,
+                                             int32_t *res_a, int32_t *res_b) {
+    return single_input_host(c, OP_KS, B, 0, u_a, u_b, res_a, res_b);
+}
+
+// a second context on the same GPU sharing `primary`'s key (own stream + scratch):
+// used for per-thread lanes of the Tier-1 API
+TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
+    TfheAmdContext *c = new TfheAmdContext();
+    c->device = primary->device;
+    c->key = primary->key;
+    c->shared_key = true;
+    if (hipSetDevice(c->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        tfhe_amd_reserve(c, 64) != TFHE_AMD_OK) {
+        tfhe_amd_context_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+extern "C" const char *tfhe_amd_version(void) { return "tfhe_amd gfx950 ntt2x30 br-v1 ks-v1"; }

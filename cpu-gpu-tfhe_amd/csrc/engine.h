@@ -1,0 +1,41 @@
+// engine.h — internal device-engine interface (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "params.h"
+#include "ntt_tables.h"
+
+namespace tfhe_amd {
+
+// Key material of one cloud key resident on one GPU.
+struct DeviceKey {
+    int device = -1;
+    uint32_t *bk_ntt = nullptr;   // [kn][2 primes][kKpl][2][kN], Montgomery form, 1/N folded
+    int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
+    NttTables *tables = nullptr;  // device copy
+    bool has_bk = false;
+};
+
+// x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
+struct BrInput {
+    const int32_t *x_a, *x_b;
+    const int32_t *y_a, *y_b;
+    int32_t c, sa, sb;
+};
+
+// BK conversion (coefficient -> NTT domain) on the device; d_bk_coef = [kn][4][2][kN]
+hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const NttTables *d_tab,
+                            hipStream_t s);
+// Blind rotation + sample extraction for `halves` x B ciphertexts: ciphertext g of half h
+// reads in[h] at index g and writes u[h*B + g] (u_a row stride kN).
+hipError_t launch_blind_rotate(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                               int32_t *u_a, int32_t *u_b, hipStream_t s);
+// Debug: `iters` CMux steps on explicit accumulators acc [B][2][kN] with bara [B][iters].
+hipError_t launch_blind_rotate_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                     const int32_t *bara, hipStream_t s);
+// Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).
+hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,
+                            const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,
+                            int32_t *res_a, int32_t *res_b, hipStream_t s);
+
+}  // namespace tfhe_amd

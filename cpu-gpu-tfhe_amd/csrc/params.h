@@ -1,0 +1,36 @@
+// params.h — the default gate-bootstrapping parameter set, fixed at compile time.
+// new_default_gate_bootstrapping_parameters (gpuParallel/tfhe_gate_bootstrapping.cu:25-49),
+// TGswParams ctor (tgsw.cu:7-29), key-switch layout (lwekeyswitch.cu:3-18).
+#pragma once
+#include <cstdint>
+
+namespace tfhe_amd {
+
+constexpr int kN = 1024;          // ring degree (TLWE N)
+constexpr int kLogN = 10;
+constexpr int k2N = 2 * kN;
+constexpr int kn = 500;           // LWE dimension (in/out)
+constexpr int kK = 1;             // TLWE mask polynomials
+constexpr int kL = 2;             // gadget decomposition length
+constexpr int kBgbit = 10;        // log2 Bg
+constexpr int kKpl = (kK + 1) * kL;   // 4 TGSW rows
+constexpr int kKsT = 8;           // key-switch digits
+constexpr int kKsBasebit = 2;     // key-switch base 4
+constexpr int kKsBase = 1 << kKsBasebit;
+constexpr uint32_t kDecompOffset = 512u * ((1u << 22) + (1u << 12));   // 2149580800
+constexpr uint32_t kKsPrecOffset = 1u << (32 - (1 + kKsBasebit * kKsT)); // 2^15
+
+// Device key-switch key rows: for each (i<1024, j<8) the three non-zero digits h=1..3,
+// each row = 500 a-coefficients, b, zero padding to 512 int32 (2 KB, 16-B aligned).
+constexpr int kKsRow = 512;
+
+// The exact external product: 2-prime CRT NTT, q < 2^30, q == 1 mod 2N.
+// q0*q1 ~ 2^60 > 2 * (4 rows * 1024 * 512 * 2^31) = 2^53 (SURVEY.md §7.3 option (i)).
+constexpr uint32_t kQ[2] = {1073707009u, 1073698817u};
+
+// standard deviations, tfhe_gate_bootstrapping.cu:36-38 (mulBySqrtTwoOverPi :22)
+constexpr double kKsStdev = 2.4349504419032758e-05;   // sqrt(2/pi) * 2^-15
+constexpr double kBkStdev = 7.180961047225788e-09;    // sqrt(2/pi) * 9e-9
+constexpr double kMaxStdev = 0.012466946262544772;    // sqrt(2/pi) * 2^-4 / 4
+
+}  // namespace tfhe_amd

@@ -1,0 +1,711 @@
+// tfhe_api.cpp — the TFHE C API (Tier-1) over the MI355X engine.
+//
+// The drop-in boundary of SURVEY.md §8(b): the functions cpuParallel/Cipher.cpp and
+// cloud.cpp call from libtfhe (bootsXXX, tfhe_bootstrap_(woKS_)FFT, lweKeySwitch, the
+// key/ciphertext lifecycle and the LWE helpers).  Structs are allocated with the
+// reference's layouts (include/tfhe/tfhe.h); the bootstrapped operations run on the GPU
+// through a device context cached per key (engine.cpp).  Host-only pieces (key
+// generation, encryption, linear LWE ops) restate the reference's CPU code and keep its
+// RNG: std::default_random_engine seeded by tfhe_random_generator_setSeed
+// (numeric-functions.cu:11-19), drawn in the reference's order.
+//
+// Reentrancy: every calling thread gets its own "lane" (stream + scratch) per key, so
+// OpenMP callers (Cipher.cpp:116-120, cloud.cpp:390-393) run concurrently; the reference's
+// global FFT scratch (lagrangehalfc_impl.cu:4) has no counterpart here.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <unordered_map>
+#include <vector>
+
+#include "params.h"
+#include "../../include/tfhe/tfhe.h"
+#include "../../include/tfhe_amd.h"
+
+using namespace tfhe_amd;
+
+TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary);   // engine.cpp
+
+// ------------------------------------------------------------------ numerics
+// numeric-functions.cu:11-77
+
+static std::default_random_engine generator;
+static std::uniform_int_distribution<Torus32> uniformTorus32_distrib(INT32_MIN, INT32_MAX);
+static std::mutex g_rng_mu;   // the reference RNG is global and not thread safe; we lock it
+
+EXPORT void die_dramatically(const char *message) {
+    std::cerr << message << std::endl;
+    abort();
+}
+
+EXPORT void tfhe_random_generator_setSeed(uint32_t *values, int size) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    std::seed_seq seeds(values, values + size);
+    generator.seed(seeds);
+}
+
+EXPORT Torus32 dtot32(double d) { return int32_t(int64_t((d - int64_t(d)) * 4294967296.0)); }
+EXPORT double t32tod(Torus32 x) { return double(x) / 4294967296.0; }
+
+static Torus32 gaussian32_nolock(Torus32 message, double sigma) {
+    std::normal_distribution<double> distribution(0., sigma);   // fresh per draw, as :24
+    double err = distribution(generator);
+    return (Torus32)((uint32_t)message + (uint32_t)dtot32(err));
+}
+EXPORT Torus32 gaussian32(Torus32 message, double sigma) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    return gaussian32_nolock(message, sigma);
+}
+
+EXPORT Torus32 approxPhase(Torus32 phase, int Msize) {
+    uint64_t interv = ((UINT64_C(1) << 63) / Msize) * 2;
+    uint64_t half_interval = interv / 2;
+    uint64_t phase64 = (uint64_t(uint32_t(phase)) << 32) + half_interval;
+    phase64 -= phase64 % interv;
+    return int32_t(phase64 >> 32);
+}
+EXPORT int modSwitchFromTorus32(Torus32 phase, int Msize) {
+    uint64_t interv = ((UINT64_C(1) << 63) / Msize) * 2;
+    uint64_t half_interval = interv / 2;
+    uint64_t phase64 = (uint64_t(uint32_t(phase)) << 32) + half_interval;
+    return int(phase64 / interv);
+}
+EXPORT Torus32 modSwitchToTorus32(int mu, int Msize) {
+    uint64_t interv = ((UINT64_C(1) << 63) / Msize) * 2;
+    uint64_t phase64 = uint64_t(int64_t(mu)) * interv;
+    return Torus32(uint32_t(phase64 >> 32));
+}
+
+// ------------------------------------------------------------------ params
+// tfhe_gate_bootstrapping.cu:25-55; tgsw.cu:7-29; tlwe.cu (extracted params n = k N)
+
+struct ParamsImpl {
+    LweParams in_out{kn, kKsStdev, kMaxStdev};
+    TLweParams accum{kN, kK, kBkStdev, kMaxStdev, LweParams{kN * kK, kBkStdev, kMaxStdev}};
+    Torus32 h[kL];
+    TGswParams tgsw{kL, kBgbit, 1 << kBgbit, (1 << kBgbit) / 2, (1u << kBgbit) - 1, &accum, kKpl, h, kDecompOffset};
+    TFheGateBootstrappingParameterSet set{kKsT, kKsBasebit, &in_out, &tgsw};
+    ParamsImpl() {
+        for (int i = 0; i < kL; ++i) h[i] = Torus32(1u << (32 - (i + 1) * kBgbit));
+    }
+};
+
+static std::mutex g_params_mu;
+static std::map<const TFheGateBootstrappingParameterSet *, ParamsImpl *> g_params;
+
+EXPORT TFheGateBootstrappingParameterSet *new_default_gate_bootstrapping_parameters(int minimum_lambda) {
+    if (minimum_lambda > 128)
+        die_dramatically("Sorry, for now, the parameters are only implemented for about 128bit of security!");
+    ParamsImpl *p = new ParamsImpl();
+    std::lock_guard<std::mutex> lk(g_params_mu);
+    g_params[&p->set] = p;
+    return &p->set;
+}
+
+EXPORT void delete_gate_bootstrapping_parameters(TFheGateBootstrappingParameterSet *params) {
+    std::lock_guard<std::mutex> lk(g_params_mu);
+    auto it = g_params.find(params);
+    if (it != g_params.end()) {
+        delete it->second;
+        g_params.erase(it);
+    }
+}
+
+// ------------------------------------------------------------------ LWE samples
+// lwesamples.cu, lwe-functions.cu:21-291
+
+EXPORT LweSample *new_LweSample_array(int nbelts, const LweParams *params) {
+    LweSample *s = (LweSample *)malloc(sizeof(LweSample) * (size_t)(nbelts > 0 ? nbelts : 1));
+    for (int i = 0; i < nbelts; i++) {
+        s[i].a = (Torus32 *)calloc((size_t)params->n, sizeof(Torus32));
+        s[i].b = 0;
+        s[i].current_variance = 0.;
+    }
+    return s;
+}
+EXPORT LweSample *new_LweSample(const LweParams *params) { return new_LweSample_array(1, params); }
+EXPORT void delete_LweSample_array(int nbelts, LweSample *obj) {
+    if (!obj) return;
+    for (int i = 0; i < nbelts; i++) free(obj[i].a);
+    free(obj);
+}
+EXPORT void delete_LweSample(LweSample *obj) { delete_LweSample_array(1, obj); }
+
+EXPORT LweSample *new_gate_bootstrapping_ciphertext(const TFheGateBootstrappingParameterSet *params) {
+    return new_LweSample(params->in_out_params);
+}
+EXPORT LweSample *new_gate_bootstrapping_ciphertext_array(int nbelems, const TFheGateBootstrappingParameterSet *params) {
+    return new_LweSample_array(nbelems, params->in_out_params);
+}
+EXPORT void delete_gate_bootstrapping_ciphertext(LweSample *sample) { delete_LweSample(sample); }
+EXPORT void delete_gate_bootstrapping_ciphertext_array(int nbelems, LweSample *samples) {
+    delete_LweSample_array(nbelems, samples);
+}
+
+static LweKey *new_LweKey(const LweParams *params) {
+    LweKey *k = (LweKey *)malloc(sizeof(LweKey));
+    *const_cast<const LweParams **>(&k->params) = params;
+    k->key = (int *)calloc((size_t)params->n, sizeof(int));
+    return k;
+}
+static void delete_LweKey(LweKey *k) {
+    if (!k) return;
+    free(k->key);
+    free(k);
+}
+
+static void lweKeyGen_nolock(LweKey *result) {
+    std::uniform_int_distribution<int> distribution(0, 1);
+    for (int i = 0; i < result->params->n; i++) result->key[i] = distribution(generator);
+}
+EXPORT void lweKeyGen(LweKey *result) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    lweKeyGen_nolock(result);
+}
+
+static void lweSymEncrypt_nolock(LweSample *result, Torus32 message, double alpha, const LweKey *key) {
+    const int n = key->params->n;
+    uint32_t b = (uint32_t)gaussian32_nolock(message, alpha);
+    for (int i = 0; i < n; ++i) {
+        result->a[i] = uniformTorus32_distrib(generator);
+        b += (uint32_t)result->a[i] * (uint32_t)key->key[i];
+    }
+    result->b = (Torus32)b;
+    result->current_variance = alpha * alpha;
+}
+EXPORT void lweSymEncrypt(LweSample *result, Torus32 message, double alpha, const LweKey *key) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    lweSymEncrypt_nolock(result, message, alpha, key);
+}
+
+static void lweSymEncryptWithExternalNoise_nolock(LweSample *result, Torus32 message, double noise, double alpha,
+                                                  const LweKey *key) {
+    const int n = key->params->n;
+    uint32_t b = (uint32_t)message + (uint32_t)dtot32(noise);
+    for (int i = 0; i < n; ++i) {
+        result->a[i] = uniformTorus32_distrib(generator);
+        b += (uint32_t)result->a[i] * (uint32_t)key->key[i];
+    }
+    result->b = (Torus32)b;
+    result->current_variance = alpha * alpha;
+}
+EXPORT void lweSymEncryptWithExternalNoise(LweSample *result, Torus32 message, double noise, double alpha,
+                                           const LweKey *key) {
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    lweSymEncryptWithExternalNoise_nolock(result, message, noise, alpha, key);
+}
+
+EXPORT Torus32 lwePhase(const LweSample *sample, const LweKey *key) {
+    uint32_t axs = 0;
+    for (int i = 0; i < key->params->n; ++i) axs += (uint32_t)sample->a[i] * (uint32_t)key->key[i];
+    return (Torus32)((uint32_t)sample->b - axs);
+}
+EXPORT Torus32 lweSymDecrypt(const LweSample *sample, const LweKey *key, const int Msize) {
+    return approxPhase(lwePhase(sample, key), Msize);
+}
+
+EXPORT void lweClear(LweSample *r, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = 0;
+    r->b = 0;
+    r->current_variance = 0.;
+}
+EXPORT void lweCopy(LweSample *r, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = s->a[i];
+    r->b = s->b;
+    r->current_variance = s->current_variance;
+}
+EXPORT void lweNegate(LweSample *r, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = (Torus32)(0u - (uint32_t)s->a[i]);
+    r->b = (Torus32)(0u - (uint32_t)s->b);
+    r->current_variance = s->current_variance;
+}
+EXPORT void lweNoiselessTrivial(LweSample *r, Torus32 mu, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = 0;
+    r->b = mu;
+    r->current_variance = 0.;
+}
+EXPORT void lweAddTo(LweSample *r, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = (Torus32)((uint32_t)r->a[i] + (uint32_t)s->a[i]);
+    r->b = (Torus32)((uint32_t)r->b + (uint32_t)s->b);
+    r->current_variance += s->current_variance;
+}
+EXPORT void lweSubTo(LweSample *r, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = (Torus32)((uint32_t)r->a[i] - (uint32_t)s->a[i]);
+    r->b = (Torus32)((uint32_t)r->b - (uint32_t)s->b);
+    r->current_variance += s->current_variance;
+}
+EXPORT void lweAddMulTo(LweSample *r, int p, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = (Torus32)((uint32_t)r->a[i] + (uint32_t)p * (uint32_t)s->a[i]);
+    r->b = (Torus32)((uint32_t)r->b + (uint32_t)p * (uint32_t)s->b);
+    r->current_variance += (p * p) * s->current_variance;
+}
+EXPORT void lweSubMulTo(LweSample *r, int p, const LweSample *s, const LweParams *params) {
+    for (int i = 0; i < params->n; ++i) r->a[i] = (Torus32)((uint32_t)r->a[i] - (uint32_t)p * (uint32_t)s->a[i]);
+    r->b = (Torus32)((uint32_t)r->b - (uint32_t)p * (uint32_t)s->b);
+    r->current_variance += (p * p) * s->current_variance;
+}
+
+// ------------------------------------------------------------------ keys
+
+// Private owners behind the public (reference-layout) structs.  The bootstrapping key is
+// kept as one contiguous coefficient-domain block [kn][kpl][k+1][N] — the layout the device
+// upload consumes — and the public TGswSample/TLweSample/TorusPolynomial views point into it.
+struct BkImpl {
+    LweBootstrappingKey pub;
+    std::vector<int32_t> coef;                // [kn][4][2][kN]
+    std::vector<TorusPolynomial> polys;       // kn*4*2 views
+    std::vector<TLweSample> rows;             // kn*4
+    std::vector<TLweSample *> blocs;          // kn*(k+1) bloc pointers
+    std::vector<TGswSample> gsw;              // kn
+    LweKeySwitchKey *ks;
+};
+
+struct KskImpl {
+    LweKeySwitchKey pub;
+    std::vector<int32_t> a;                   // [kN*8*4][kn]
+    std::vector<LweSample> samples;           // kN*8*4
+    std::vector<LweSample *> l1;              // kN*8
+    std::vector<LweSample **> l0;             // kN
+};
+
+struct BkFFTImpl {
+    LweBootstrappingKeyFFT pub;
+    std::vector<int32_t> bk_coef;             // [kn][4][2][kN]   (NTT conversion happens on the GPU)
+    LweKeySwitchKey *ks;                      // deep copy (owned)
+};
+
+static KskImpl *ksk_of(const LweKeySwitchKey *k) { return reinterpret_cast<KskImpl *>(const_cast<LweKeySwitchKey *>(k)); }
+static BkFFTImpl *bkfft_of(const LweBootstrappingKeyFFT *k) {
+    return reinterpret_cast<BkFFTImpl *>(const_cast<LweBootstrappingKeyFFT *>(k));
+}
+static BkImpl *bk_of(const LweBootstrappingKey *k) { return reinterpret_cast<BkImpl *>(const_cast<LweBootstrappingKey *>(k)); }
+
+static LweKeySwitchKey *new_ksk(const LweParams *out_params) {
+    KskImpl *k = new KskImpl{LweKeySwitchKey{kN, kKsT, kKsBasebit, kKsBase, out_params, nullptr, nullptr, nullptr},
+                             {}, {}, {}, {}};
+    const size_t ns = (size_t)kN * kKsT * kKsBase;
+    k->a.assign(ns * kn, 0);
+    k->samples.resize(ns);
+    for (size_t s = 0; s < ns; s++) k->samples[s] = LweSample{k->a.data() + s * kn, 0, 0.};
+    k->l1.resize((size_t)kN * kKsT);
+    for (size_t p = 0; p < k->l1.size(); p++) k->l1[p] = k->samples.data() + kKsBase * p;
+    k->l0.resize(kN);
+    for (int p = 0; p < kN; p++) k->l0[p] = k->l1.data() + kKsT * p;
+    k->pub.ks0_raw = k->samples.data();
+    k->pub.ks1_raw = k->l1.data();
+    k->pub.ks = k->l0.data();
+    return &k->pub;
+}
+static void delete_ksk(LweKeySwitchKey *k) { delete ksk_of(k); }
+
+// flat [kN][8][4][kn+1] view of any LweKeySwitchKey (ours or foreign-built)
+static void ksk_flatten(const LweKeySwitchKey *ks, int32_t *out) {
+    for (int i = 0; i < kN; i++)
+        for (int j = 0; j < kKsT; j++)
+            for (int h = 0; h < kKsBase; h++) {
+                const LweSample &s = ks->ks[i][j][h];
+                int32_t *dst = out + (((size_t)i * kKsT + j) * kKsBase + h) * (kn + 1);
+                memcpy(dst, s.a, sizeof(int32_t) * kn);
+                dst[kn] = s.b;
+            }
+}
+
+static LweBootstrappingKey *new_bk(const ParamsImpl *P) {
+    BkImpl *k = new BkImpl{LweBootstrappingKey{&P->in_out, &P->tgsw, &P->accum, &P->accum.extracted_lweparams,
+                                               nullptr, nullptr},
+                           {}, {}, {}, {}, {}, nullptr};
+    k->coef.assign((size_t)kn * kKpl * 2 * kN, 0);
+    k->polys.reserve((size_t)kn * kKpl * 2);
+    for (size_t p = 0; p < (size_t)kn * kKpl * 2; p++) k->polys.push_back(TorusPolynomial{kN, k->coef.data() + p * kN});
+    k->rows.reserve((size_t)kn * kKpl);
+    for (size_t r = 0; r < (size_t)kn * kKpl; r++)
+        k->rows.push_back(TLweSample{&k->polys[r * 2], &k->polys[r * 2 + 1], 0., kK});
+    k->blocs.resize((size_t)kn * (kK + 1));
+    for (int i = 0; i < kn; i++)
+        for (int b = 0; b <= kK; b++) k->blocs[(size_t)i * (kK + 1) + b] = &k->rows[(size_t)i * kKpl + b * kL];
+    k->gsw.reserve(kn);
+    for (int i = 0; i < kn; i++)
+        k->gsw.push_back(TGswSample{&k->rows[(size_t)i * kKpl], &k->blocs[(size_t)i * (kK + 1)], kK, kL});
+    k->ks = new_ksk(&P->in_out);
+    k->pub.bk = k->gsw.data();
+    k->pub.ks = k->ks;
+    return &k->pub;
+}
+static void delete_bk(LweBootstrappingKey *k) {
+    if (!k) return;
+    BkImpl *b = bk_of(k);
+    delete_ksk(b->ks);
+    delete b;
+}
+
+// coefficient BK of any LweBootstrappingKey -> flat [kn][4][2][kN]
+static void bk_flatten(const LweBootstrappingKey *bk, int32_t *out) {
+    for (int i = 0; i < kn; i++)
+        for (int p = 0; p < kKpl; p++)
+            for (int c = 0; c <= kK; c++)
+                memcpy(out + (((size_t)i * kKpl + p) * 2 + c) * kN, bk->bk[i].all_sample[p].a[c].coefsT,
+                       sizeof(int32_t) * kN);
+}
+
+// new_LweBootstrappingKeyFFT (lwe-bootstrapping-functions-fft.cu:2201 -> :60-89): copy the KSK,
+// keep the coefficient BK for the device-side NTT conversion.
+static LweBootstrappingKeyFFT *new_bkfft(const LweBootstrappingKey *bk) {
+    BkFFTImpl *f = new BkFFTImpl{LweBootstrappingKeyFFT{bk->in_out_params, bk->bk_params, bk->accum_params,
+                                                        bk->extract_params, nullptr, nullptr},
+                                 {}, nullptr};
+    f->bk_coef.resize((size_t)kn * kKpl * 2 * kN);
+    bk_flatten(bk, f->bk_coef.data());
+    f->ks = new_ksk(bk->in_out_params);
+    std::vector<int32_t> flat((size_t)kN * kKsT * kKsBase * (kn + 1));
+    ksk_flatten(bk->ks, flat.data());
+    KskImpl *dst = ksk_of(f->ks);
+    for (size_t s = 0; s < dst->samples.size(); s++) {
+        memcpy(dst->samples[s].a, flat.data() + s * (kn + 1), sizeof(int32_t) * kn);
+        dst->samples[s].b = flat[s * (kn + 1) + kn];
+        dst->samples[s].current_variance = bk->ks->ks0_raw[s].current_variance;
+    }
+    *const_cast<const LweKeySwitchKey **>(&f->pub.ks) = f->ks;
+    *const_cast<const TGswSampleFFT **>(&f->pub.bkFFT) = reinterpret_cast<const TGswSampleFFT *>(f);
+    return &f->pub;
+}
+
+static void forget_device_keys(const void *k1, const void *k2);
+
+static void delete_bkfft(LweBootstrappingKeyFFT *k) {
+    if (!k) return;
+    BkFFTImpl *f = bkfft_of(k);
+    forget_device_keys(k, f->ks);
+    delete_ksk(f->ks);
+    delete f;
+}
+
+struct TGswKeyImpl {
+    TGswKey pub;
+    std::vector<int> coefs;
+    IntPolynomial poly;
+};
+
+// lweCreateKeySwitchKey (lwe-keyswitch-functions.cu:890-942)
+static void create_ksk_nolock(LweKeySwitchKey *result, const int *in_key /*kN*/, const LweKey *out_key) {
+    const int n = result->n, t = result->t, basebit = result->basebit, base = 1 << basebit;
+    const double alpha = out_key->params->alpha_min;
+    const int sizeks = n * t * (base - 1);
+    std::vector<double> noise(sizeks);
+    double err = 0;
+    for (int i = 0; i < sizeks; ++i) {
+        std::normal_distribution<double> distribution(0., alpha);
+        noise[i] = distribution(generator);
+        err += noise[i];
+    }
+    err = err / sizeks;
+    for (int i = 0; i < sizeks; ++i) noise[i] -= err;
+    int index = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < t; ++j) {
+            lweNoiselessTrivial(&result->ks[i][j][0], 0, out_key->params);
+            for (int h = 1; h < base; ++h) {
+                Torus32 mess = (Torus32)((uint32_t)(in_key[i] * h) * (1u << (32 - (j + 1) * basebit)));
+                lweSymEncryptWithExternalNoise_nolock(&result->ks[i][j][h], mess, noise[index], alpha, out_key);
+                index += 1;
+            }
+        }
+}
+
+// tLweSymEncryptZero (tlwe-functions.cu:26-38) with an EXACT b += key * a (the reference
+// uses its FFT multiply here, polynomials_arithmetic.h:112-114; key generation is
+// client side and off the hot path)
+static void tlwe_encrypt_zero_nolock(TLweSample *r, double alpha, const int *key /*kN binary*/) {
+    uint32_t *b = (uint32_t *)r->b->coefsT;
+    for (int j = 0; j < kN; ++j) b[j] = (uint32_t)gaussian32_nolock(0, alpha);
+    uint32_t *a = (uint32_t *)r->a[0].coefsT;
+    for (int j = 0; j < kN; ++j) a[j] = (uint32_t)uniformTorus32_distrib(generator);   // torusPolynomialUniform
+    for (int s = 0; s < kN; ++s) {
+        if (!key[s]) continue;           // b += X^s * a (negacyclic)
+        for (int i = 0; i < s; ++i) b[i] -= a[i - s + kN];
+        for (int i = s; i < kN; ++i) b[i] += a[i - s];
+    }
+    r->current_variance = alpha * alpha;
+}
+
+EXPORT TFheGateBootstrappingSecretKeySet *
+new_random_gate_bootstrapping_secret_keyset(const TFheGateBootstrappingParameterSet *params) {
+    const ParamsImpl *P;
+    {
+        std::lock_guard<std::mutex> lk(g_params_mu);
+        auto it = g_params.find(params);
+        if (it == g_params.end()) die_dramatically("tfhe_amd: unknown parameter set");
+        P = it->second;
+    }
+    std::lock_guard<std::mutex> lk(g_rng_mu);
+    LweKey *lwe_key = new_LweKey(params->in_out_params);
+    lweKeyGen_nolock(lwe_key);                                              // :60
+    TGswKeyImpl *gk = new TGswKeyImpl{TGswKey{&P->tgsw, &P->accum, nullptr, TLweKey{&P->accum, nullptr}},
+                                      std::vector<int>(kN), IntPolynomial{kN, nullptr}};
+    gk->poly.coefs = gk->coefs.data();
+    gk->pub.key = &gk->poly;
+    gk->pub.tlwe_key.key = &gk->poly;
+    {   // tGswKeyGen -> tLweKeyGen (tlwe-functions.cu:15-23)
+        std::uniform_int_distribution<int> distribution(0, 1);
+        for (int j = 0; j < kN; ++j) gk->coefs[j] = distribution(generator);
+    }
+    // tfhe_createLweBootstrappingKey (lwe-bootstrapping-functions.cu:185-217)
+    LweBootstrappingKey *bk = new_bk(P);
+    create_ksk_nolock(bk->ks, gk->coefs.data(), lwe_key);   // extracted key = tlwe key coefs (k = 1)
+    const double alpha = P->accum.alpha_min;
+    for (int i = 0; i < kn; i++) {
+        TGswSample *g = &bk->bk[i];
+        for (int p = 0; p < kKpl; ++p) tlwe_encrypt_zero_nolock(&g->all_sample[p], alpha, gk->coefs.data());
+        // tGswAddMuIntH (tgsw-functions.cu:114-124)
+        for (int bloc = 0; bloc <= kK; ++bloc)
+            for (int l = 0; l < kL; l++) {
+                Torus32 *c0 = &g->bloc_sample[bloc][l].a[bloc].coefsT[0];
+                *c0 = (Torus32)((uint32_t)*c0 + (uint32_t)lwe_key->key[i] * (uint32_t)P->h[l]);
+            }
+    }
+    LweBootstrappingKeyFFT *bkfft = new_bkfft(bk);
+    return new TFheGateBootstrappingSecretKeySet{params, lwe_key, &gk->pub,
+                                                 TFheGateBootstrappingCloudKeySet{params, bk, bkfft}};
+}
+
+EXPORT void delete_gate_bootstrapping_secret_keyset(TFheGateBootstrappingSecretKeySet *keyset) {
+    if (!keyset) return;
+    delete_bkfft(const_cast<LweBootstrappingKeyFFT *>(keyset->cloud.bkFFT));
+    delete_bk(const_cast<LweBootstrappingKey *>(keyset->cloud.bk));
+    delete reinterpret_cast<TGswKeyImpl *>(const_cast<TGswKey *>(keyset->tgsw_key));
+    delete_LweKey(const_cast<LweKey *>(keyset->lwe_key));
+    delete keyset;
+}
+
+EXPORT void delete_gate_bootstrapping_cloud_keyset(TFheGateBootstrappingCloudKeySet *keyset) {
+    if (!keyset) return;
+    delete_bkfft(const_cast<LweBootstrappingKeyFFT *>(keyset->bkFFT));
+    delete_bk(const_cast<LweBootstrappingKey *>(keyset->bk));
+    delete keyset;
+}
+
+EXPORT void bootsSymEncrypt(LweSample *result, int message, const TFheGateBootstrappingSecretKeySet *key) {
+    Torus32 _1s8 = modSwitchToTorus32(1, 8);
+    Torus32 mu = message ? _1s8 : -_1s8;
+    double alpha = key->params->in_out_params->alpha_min;
+    lweSymEncrypt(result, mu, alpha, key->lwe_key);
+}
+EXPORT int bootsSymDecrypt(const LweSample *sample, const TFheGateBootstrappingSecretKeySet *key) {
+    Torus32 mu = lwePhase(sample, key->lwe_key);
+    return mu > 0 ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ device contexts
+
+static std::atomic<int> g_default_device{0};
+
+struct KeyEntry {
+    uint64_t id;
+    const LweKeySwitchKey *ks = nullptr;
+    TfheAmdContext *primary = nullptr;
+    std::vector<TfheAmdContext *> lanes;
+    std::mutex mu;
+};
+static std::mutex g_reg_mu;
+static std::unordered_map<const void *, std::shared_ptr<KeyEntry>> g_reg;   // bkFFT or KSK -> entry
+static std::atomic<uint64_t> g_next_id{1};
+
+static std::shared_ptr<KeyEntry> entry_for(const LweBootstrappingKeyFFT *bkfft, const LweKeySwitchKey *ks) {
+    const void *k = bkfft ? (const void *)bkfft : (const void *)ks;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(k);
+    if (it != g_reg.end()) return it->second;
+    if (!bkfft) {   // a KSK that belongs to a registered bkFFT shares its context
+        for (auto &kv : g_reg)
+            if (kv.second->ks == ks) return kv.second;
+    }
+    std::vector<int32_t> flat_ks((size_t)kN * kKsT * kKsBase * (kn + 1));
+    const int32_t *bk_coef = nullptr;
+    if (bkfft) {
+        bk_coef = bkfft_of(bkfft)->bk_coef.data();
+        ksk_flatten(bkfft->ks, flat_ks.data());
+    } else {
+        ksk_flatten(ks, flat_ks.data());
+    }
+    auto e = std::make_shared<KeyEntry>();
+    e->id = g_next_id++;
+    e->ks = bkfft ? bkfft->ks : ks;
+    int rc = tfhe_amd_context_create_raw(bk_coef, flat_ks.data(), g_default_device.load(), &e->primary);
+    if (rc != TFHE_AMD_OK) {
+        fprintf(stderr, "tfhe_amd: cannot create the device context (rc=%d): no usable MI355X/HIP device\n", rc);
+        die_dramatically("tfhe_amd: GPU engine unavailable");
+    }
+    g_reg[k] = e;
+    return e;
+}
+
+static void forget_device_keys(const void *k1, const void *k2) {
+    std::vector<std::shared_ptr<KeyEntry>> dead;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (const void *k : {k1, k2}) {
+            auto it = g_reg.find(k);
+            if (it != g_reg.end()) {
+                dead.push_back(it->second);
+                g_reg.erase(it);
+            }
+        }
+    }
+    for (auto &e : dead) {
+        std::lock_guard<std::mutex> lk(e->mu);
+        for (auto *l : e->lanes) tfhe_amd_context_destroy(l);
+        e->lanes.clear();
+        tfhe_amd_context_destroy(e->primary);
+        e->primary = nullptr;
+    }
+}
+
+// this thread's lane (own stream + scratch) on the key's device
+static TfheAmdContext *lane_for(const LweBootstrappingKeyFFT *bkfft, const LweKeySwitchKey *ks) {
+    thread_local std::unordered_map<uint64_t, TfheAmdContext *> lanes;
+    std::shared_ptr<KeyEntry> e = entry_for(bkfft, ks);
+    auto it = lanes.find(e->id);
+    if (it != lanes.end()) return it->second;
+    std::lock_guard<std::mutex> lk(e->mu);
+    TfheAmdContext *l = tfhe_amd_context_lane(e->primary);
+    if (!l) die_dramatically("tfhe_amd: cannot create a per-thread GPU lane");
+    e->lanes.push_back(l);
+    lanes[e->id] = l;
+    return l;
+}
+
+EXPORT int tfhe_amd_set_default_device(int device) {
+    if (device < 0) return TFHE_AMD_E_ARG;
+    g_default_device = device;
+    return TFHE_AMD_OK;
+}
+
+EXPORT int tfhe_amd_context_create(const TFheGateBootstrappingCloudKeySet *bk, int device, TfheAmdContext **out) {
+    if (!bk || !bk->bkFFT || !out) return TFHE_AMD_E_ARG;
+    std::vector<int32_t> flat_ks((size_t)kN * kKsT * kKsBase * (kn + 1));
+    ksk_flatten(bk->bkFFT->ks, flat_ks.data());
+    return tfhe_amd_context_create_raw(bkfft_of(bk->bkFFT)->bk_coef.data(), flat_ks.data(), device, out);
+}
+
+EXPORT int tfhe_amd_export_bk(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out) {
+    if (!bk || !bk->bk || !out) return TFHE_AMD_E_ARG;
+    bk_flatten(bk->bk, out);
+    return TFHE_AMD_OK;
+}
+EXPORT int tfhe_amd_export_ksk(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out) {
+    if (!bk || !bk->bkFFT || !out) return TFHE_AMD_E_ARG;
+    ksk_flatten(bk->bkFFT->ks, out);
+    return TFHE_AMD_OK;
+}
+EXPORT int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out) {
+    if (!key || !out) return TFHE_AMD_E_ARG;
+    memcpy(out, key->lwe_key->key, sizeof(int32_t) * kn);
+    return TFHE_AMD_OK;
+}
+
+EXPORT int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out) {
+    if (!key || !out) return TFHE_AMD_E_ARG;
+    memcpy(out, key->tgsw_key->tlwe_key.key[0].coefs, sizeof(int32_t) * kN);
+    return TFHE_AMD_OK;
+}
+
+// ------------------------------------------------------------------ bootstrapping API
+
+static void check(int rc, const char *what) {
+    if (rc != TFHE_AMD_OK) {
+        fprintf(stderr, "tfhe_amd: %s failed (rc=%d)\n", what, rc);
+        die_dramatically("tfhe_amd: GPU engine error");
+    }
+}
+
+EXPORT void tfhe_bootstrap_woKS_FFT(LweSample *result, const LweBootstrappingKeyFFT *bk, Torus32 mu,
+                                    const LweSample *x) {
+    TfheAmdContext *l = lane_for(bk, nullptr);
+    check(tfhe_amd_bootstrap_woks_batch_host(l, 1, mu, x->a, &x->b, result->a, &result->b), "tfhe_bootstrap_woKS_FFT");
+    result->current_variance = 0.;   // bookkeeping only (excluded from parity)
+}
+
+EXPORT void tfhe_bootstrap_FFT(LweSample *result, const LweBootstrappingKeyFFT *bk, Torus32 mu, const LweSample *x) {
+    TfheAmdContext *l = lane_for(bk, nullptr);
+    check(tfhe_amd_bootstrap_batch_host(l, 1, mu, x->a, &x->b, result->a, &result->b), "tfhe_bootstrap_FFT");
+    result->current_variance = 0.;
+}
+
+EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const LweSample *sample) {
+    TfheAmdContext *l = lane_for(nullptr, ks);
+    check(tfhe_amd_keyswitch_batch_host(l, 1, sample->a, &sample->b, result->a, &result->b), "lweKeySwitch");
+    result->current_variance = 0.;
+}
+
+// ------------------------------------------------------------------ gates
+
+static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b, const LweSample *c,
+                  const TFheGateBootstrappingCloudKeySet *bk) {
+    TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
+    check(tfhe_amd_gate_batch_host(l, gate, 1, r->a, &r->b, a->a, &a->b, b->a, &b->b, c ? c->a : nullptr,
+                                   c ? &c->b : nullptr),
+          "gate");
+    r->current_variance = 0.;
+}
+
+EXPORT void bootsNAND(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_NAND, r, a, b, nullptr, bk); }
+EXPORT void bootsOR(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_OR, r, a, b, nullptr, bk); }
+EXPORT void bootsAND(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_AND, r, a, b, nullptr, bk); }
+EXPORT void bootsXOR(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_XOR, r, a, b, nullptr, bk); }
+EXPORT void bootsXNOR(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_XNOR, r, a, b, nullptr, bk); }
+EXPORT void bootsNOR(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_NOR, r, a, b, nullptr, bk); }
+EXPORT void bootsANDNY(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_ANDNY, r, a, b, nullptr, bk); }
+EXPORT void bootsANDYN(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_ANDYN, r, a, b, nullptr, bk); }
+EXPORT void bootsORNY(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_ORNY, r, a, b, nullptr, bk); }
+EXPORT void bootsORYN(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_ORYN, r, a, b, nullptr, bk); }
+EXPORT void bootsMUX(LweSample *r, const LweSample *a, const LweSample *b, const LweSample *c,
+                     const TFheGateBootstrappingCloudKeySet *bk) {
+    gate1(TFHE_GATE_MUX, r, a, b, c, bk);
+}
+
+// linear gates stay on the host (boot-gates.cu:242-267)
+EXPORT void bootsNOT(LweSample *r, const LweSample *a, const TFheGateBootstrappingCloudKeySet *bk) {
+    lweNegate(r, a, bk->params->in_out_params);
+}
+EXPORT void bootsCOPY(LweSample *r, const LweSample *a, const TFheGateBootstrappingCloudKeySet *bk) {
+    lweCopy(r, a, bk->params->in_out_params);
+}
+EXPORT void bootsCONSTANT(LweSample *r, int value, const TFheGateBootstrappingCloudKeySet *bk) {
+    const Torus32 MU = modSwitchToTorus32(1, 8);
+    lweNoiselessTrivial(r, value ? MU : -MU, bk->params->in_out_params);
+}
+
+// batched convenience over LweSample arrays (SoA staging on the host)
+EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
+                                const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk) {
+    if (!bk || !bk->bkFFT || B < 0 || !result || !a || !b) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (gate == TFHE_GATE_MUX && !c) return TFHE_AMD_E_ARG;
+    TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
+    const size_t A = (size_t)B * kn;
+    std::vector<int32_t> buf(4 * A + 4 * (size_t)B);
+    int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
+    int32_t *ab = ra + A, *bb = ab + B, *cb = bb + B, *rb = cb + B;
+    for (int i = 0; i < B; i++) {
+        memcpy(aa + (size_t)i * kn, a[i].a, kn * 4); ab[i] = a[i].b;
+        memcpy(ba + (size_t)i * kn, b[i].a, kn * 4); bb[i] = b[i].b;
+        if (c) { memcpy(ca + (size_t)i * kn, c[i].a, kn * 4); cb[i] = c[i].b; }
+    }
+    int rc = tfhe_amd_gate_batch_host(l, gate, B, ra, rb, aa, ab, ba, bb, c ? ca : nullptr, c ? cb : nullptr);
+    if (rc) return rc;
+    for (int i = 0; i < B; i++) {
+        memcpy(result[i].a, ra + (size_t)i * kn, kn * 4);
+        result[i].b = rb[i];
+        result[i].current_variance = 0.;
+    }
+    return TFHE_AMD_OK;
+}

@@ -1,0 +1,254 @@
+"""Python binding (ctypes) of libtfhe_amd.so — the MI355X TFHE gate-bootstrapping engine.
+
+Thin host-side mirror of the C ABI (include/tfhe/tfhe.h = the TFHE API cpuParallel links,
+include/tfhe_amd.h = the batched device API).  It exists for the tests and bench.py; the
+product is the C ABI itself.  Importing this module loads lib/libtfhe_amd.so and fails
+loudly if it is missing (there is no CPU fallback).
+
+Ciphertext batches are SoA numpy / torch arrays: a int32 [B][500], b int32 [B].
+"""
+import ctypes
+import os
+
+import numpy as np
+
+try:
+    # torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's): load it FIRST so
+    # that this process has one HIP runtime, shared by torch tensors and our kernels.
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - the C ABI itself does not need torch
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtfhe_amd.so")
+
+N, n_lwe, KPL, KS_T, KS_BASE = 1024, 500, 4, 8, 4
+GATES = {"NAND": 0, "OR": 1, "AND": 2, "XOR": 3, "XNOR": 4, "NOR": 5,
+         "ANDNY": 6, "ANDYN": 7, "ORNY": 8, "ORYN": 9, "MUX": 10}
+MU = 1 << 29   # modSwitchToTorus32(1, 8)
+
+_I32P = ctypes.POINTER(ctypes.c_int32)
+_VP = ctypes.c_void_p
+
+
+class TfheAmdError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise TfheAmdError(
+            f"{LIB_PATH} is missing: build it (python -c 'import __graft_entry__ as g; g.build()' "
+            "or make -C cpu-gpu-tfhe_amd). There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    L.tfhe_amd_version.restype = ctypes.c_char_p
+    L.new_default_gate_bootstrapping_parameters.restype = _VP
+    L.new_random_gate_bootstrapping_secret_keyset.restype = _VP
+    L.new_random_gate_bootstrapping_secret_keyset.argtypes = [_VP]
+    L.delete_gate_bootstrapping_secret_keyset.argtypes = [_VP]
+    L.delete_gate_bootstrapping_parameters.argtypes = [_VP]
+    L.tfhe_amd_export_bk.argtypes = [_VP, _I32P]
+    L.tfhe_amd_export_ksk.argtypes = [_VP, _I32P]
+    L.tfhe_amd_export_lwe_key.argtypes = [_VP, _I32P]
+    L.tfhe_amd_export_tlwe_key.argtypes = [_VP, _I32P]
+    L.tfhe_amd_context_create_raw.argtypes = [_I32P, _I32P, ctypes.c_int, ctypes.POINTER(_VP)]
+    L.tfhe_amd_context_create.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(_VP)]
+    L.tfhe_amd_context_destroy.argtypes = [_VP]
+    L.tfhe_amd_context_stream.restype = _VP
+    L.tfhe_amd_context_stream.argtypes = [_VP]
+    L.tfhe_amd_sync.argtypes = [_VP]
+    L.tfhe_amd_reserve.argtypes = [_VP, ctypes.c_int]
+    for f in ("tfhe_amd_gate_batch_dev",):
+        getattr(L, f).argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_VP] * 8 + [_VP]
+    L.tfhe_amd_gate_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_I32P] * 8
+    L.tfhe_amd_bootstrap_woks_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
+    L.tfhe_amd_bootstrap_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
+    L.tfhe_amd_keyswitch_batch_dev.argtypes = [_VP, ctypes.c_int] + [_VP] * 4 + [_VP]
+    L.tfhe_amd_bootstrap_woks_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_I32P] * 4
+    L.tfhe_amd_bootstrap_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_I32P] * 4
+    L.tfhe_amd_keyswitch_batch_host.argtypes = [_VP, ctypes.c_int] + [_I32P] * 4
+    L.tfhe_amd_blind_rotate_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]
+    L.tfhe_amd_profile_enable.argtypes = [_VP, ctypes.c_int]
+    L.tfhe_amd_profile_read.argtypes = [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    L.tfhe_random_generator_setSeed.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+    L.modSwitchToTorus32.restype = ctypes.c_int32
+    L.modSwitchFromTorus32.restype = ctypes.c_int
+    L.lwePhase.restype = ctypes.c_int32
+    return L
+
+
+lib = _load()
+
+
+def version():
+    return lib.tfhe_amd_version().decode()
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_I32P)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise TfheAmdError(f"{what} failed with code {rc}")
+
+
+def i32(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.int64).astype(np.int32))
+
+
+# --------------------------------------------------------------------- keys (host)
+
+class SecretKeyset:
+    """new_random_gate_bootstrapping_secret_keyset (tfhe_gate_bootstrapping.cu:57-68) seeded
+    through tfhe_random_generator_setSeed; exposes the key material as numpy arrays."""
+
+    def __init__(self, seed=(314, 1592, 657)):
+        s = (ctypes.c_uint32 * len(seed))(*seed)
+        lib.tfhe_random_generator_setSeed(s, len(seed))
+        self.params = lib.new_default_gate_bootstrapping_parameters(110)
+        self.h = lib.new_random_gate_bootstrapping_secret_keyset(self.params)
+        if not self.h:
+            raise TfheAmdError("keygen failed")
+        self.bk = np.zeros((n_lwe, KPL, 2, N), np.int32)
+        self.ksk = np.zeros((N, KS_T, KS_BASE, n_lwe + 1), np.int32)
+        self.lwe_key = np.zeros(n_lwe, np.int32)
+        _check(lib.tfhe_amd_export_bk(ctypes.c_void_p(self._cloud()), _p(self.bk)), "export_bk")
+        _check(lib.tfhe_amd_export_ksk(ctypes.c_void_p(self._cloud()), _p(self.ksk)), "export_ksk")
+        _check(lib.tfhe_amd_export_lwe_key(ctypes.c_void_p(self.h), _p(self.lwe_key)), "export_lwe_key")
+        self.tlwe_key = np.zeros(N, np.int32)
+        _check(lib.tfhe_amd_export_tlwe_key(ctypes.c_void_p(self.h), _p(self.tlwe_key)), "export_tlwe_key")
+
+    def _cloud(self):
+        # &key->cloud: TFheGateBootstrappingSecretKeySet = {params*, lwe_key*, tgsw_key*, cloud}
+        return self.h + 3 * ctypes.sizeof(ctypes.c_void_p)
+
+    @property
+    def cloud(self):
+        return self._cloud()
+
+    def close(self):
+        if self.h:
+            lib.delete_gate_bootstrapping_secret_keyset(self.h)
+            self.h = None
+
+    # numpy-side encryption with the same secret (fast path for big batches; the product's
+    # bootsSymEncrypt is covered by its own test)
+    def encrypt(self, bits, rng, stdev=2.4349504419032758e-05):
+        bits = np.asarray(bits).astype(np.int64)
+        B = bits.shape[0]
+        a = rng.integers(-2**31, 2**31, (B, n_lwe), dtype=np.int64)
+        mu = np.where(bits != 0, MU, -MU)
+        noise = np.rint(rng.normal(0.0, stdev, B) * 2**32).astype(np.int64)
+        b = (a @ self.lwe_key.astype(np.int64) + mu + noise)
+        return i32(a), i32(b)
+
+    def phase(self, a, b):
+        a = np.asarray(a).astype(np.int64)
+        ph = (np.asarray(b).astype(np.int64) - a @ self.lwe_key.astype(np.int64)) & 0xFFFFFFFF
+        return ph.astype(np.uint32).view(np.int32)
+
+    def decrypt(self, a, b):
+        return (self.phase(a, b) > 0).astype(np.int32)
+
+    def phase_extracted(self, u_a, u_b):
+        """phase of a woKS output (dimension N) under the extracted key (tLweExtractKey)."""
+        u_a = np.asarray(u_a).astype(np.int64)
+        ph = (np.asarray(u_b).astype(np.int64) - u_a @ self.tlwe_key.astype(np.int64)) & 0xFFFFFFFF
+        return ph.astype(np.uint32).view(np.int32)
+
+
+# --------------------------------------------------------------------- device context
+
+class Context:
+    """TfheAmdContext: key material of one cloud key on one GPU (tfhe_amd_context_create_raw)."""
+
+    def __init__(self, bk, ksk, device=0):
+        self.bk = i32(bk)
+        self.ksk = i32(ksk)
+        h = _VP()
+        _check(lib.tfhe_amd_context_create_raw(_p(self.bk), _p(self.ksk), int(device), ctypes.byref(h)),
+               "tfhe_amd_context_create_raw")
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.tfhe_amd_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib.tfhe_amd_context_stream(self.h)
+
+    def sync(self):
+        _check(lib.tfhe_amd_sync(self.h), "sync")
+
+    def reserve(self, B):
+        _check(lib.tfhe_amd_reserve(self.h, int(B)), "reserve")
+
+    # ---- host (numpy) batches
+    def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None):
+        g = GATES[gate] if isinstance(gate, str) else int(gate)
+        ca_a = i32(ca_a); B = ca_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_gate_batch_host(self.h, g, B, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)),
+                                            _p(i32(cb_a)), _p(i32(cb_b)),
+                                            _p(None if cc_a is None else i32(cc_a)),
+                                            _p(None if cc_b is None else i32(cc_b))), "gate_batch_host")
+        return r_a, r_b
+
+    def woks_host(self, mu, x_a, x_b):
+        x_a = i32(x_a); B = x_a.shape[0]
+        u_a = np.zeros((B, N), np.int32); u_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_bootstrap_woks_batch_host(self.h, B, int(mu), _p(x_a), _p(i32(x_b)), _p(u_a), _p(u_b)),
+               "woks_host")
+        return u_a, u_b
+
+    def bootstrap_host(self, mu, x_a, x_b):
+        x_a = i32(x_a); B = x_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_bootstrap_batch_host(self.h, B, int(mu), _p(x_a), _p(i32(x_b)), _p(r_a), _p(r_b)),
+               "bootstrap_host")
+        return r_a, r_b
+
+    def keyswitch_host(self, u_a, u_b):
+        u_a = i32(u_a); B = u_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_keyswitch_batch_host(self.h, B, _p(u_a), _p(i32(u_b)), _p(r_a), _p(r_b)),
+               "keyswitch_host")
+        return r_a, r_b
+
+    # ---- device (torch) batches: tensors must be int32 CUDA/HIP tensors, contiguous
+    def gate_dev(self, gate, res_a, res_b, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, stream=None):
+        g = GATES[gate] if isinstance(gate, str) else int(gate)
+        B = ca_a.shape[0]
+        ptr = (lambda t: None if t is None else t.data_ptr())
+        _check(lib.tfhe_amd_gate_batch_dev(self.h, g, B, ptr(res_a), ptr(res_b), ptr(ca_a), ptr(ca_b),
+                                           ptr(cb_a), ptr(cb_b), ptr(cc_a), ptr(cc_b), stream),
+               "gate_batch_dev")
+
+    def blind_rotate_dev(self, acc, bara, iters, stream=None):
+        B = acc.shape[0]
+        _check(lib.tfhe_amd_blind_rotate_dev(self.h, B, int(iters), acc.data_ptr(),
+                                             None if bara is None else bara.data_ptr(), stream),
+               "blind_rotate_dev")
+
+    def profile_enable(self, on=True):
+        _check(lib.tfhe_amd_profile_enable(self.h, int(on)), "profile_enable")
+
+    def profile_read(self):
+        br = ctypes.c_double(); ks = ctypes.c_double(); nb = ctypes.c_int(); nk = ctypes.c_int()
+        _check(lib.tfhe_amd_profile_read(self.h, ctypes.byref(br), ctypes.byref(nb), ctypes.byref(ks),
+                                         ctypes.byref(nk)), "profile_read")
+        return {"br_ms": br.value, "br_launches": nb.value, "ks_ms": ks.value, "ks_launches": nk.value}

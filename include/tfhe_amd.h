@@ -1,0 +1,133 @@
+/*
+ * tfhe_amd.h — the batched (Tier-2) C ABI of the MI355X gate-bootstrapping engine.
+ *
+ * It is the throughput path of SURVEY.md §8(b): the reference's bit-coalesced batch API
+ * (LweSample_16 = {int* a [B x n], int* b [B]}, gpuParallel/lwesamples.h:9-13) driven
+ * by bootsAND_fullGPU_n_Bit / bootsXOR_fullGPU_n_Bit / bootsMUX_fullGPU_n_Bit
+ * (gpuParallel/boot-gates.cu:2845-3024) and bootstrapAndKeySwitch_n_Bit (:2481-2629).
+ * Each entry point here replaces one of those; unlike the reference, the `b` halves live
+ * on the device too, all gates (incl. NAND/OR/NOR/AND-NY..., which the reference GPU
+ * path lacks) are supported, and results are Torus32-exact.
+ *
+ * Plain pointers and sizes only.  Ciphertext batches are SoA:
+ *   a : int32 [B][500] (row stride 500), b : int32 [B]
+ * `_dev` functions take DEVICE pointers (resident in HBM) and a hipStream_t passed as
+ * void* (NULL = the context's own stream); they enqueue and return (call
+ * tfhe_amd_sync to wait).  `_host` functions take host pointers and are synchronous.
+ * Every function returns 0 on success or a negative TFHE_AMD_E* code.
+ */
+#ifndef TFHE_AMD_H
+#define TFHE_AMD_H
+
+#include <stdint.h>
+#include "tfhe/tfhe_core.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    TFHE_AMD_OK = 0,
+    TFHE_AMD_E_ARG = -1,       /* bad argument / unknown gate / B < 0 */
+    TFHE_AMD_E_HIP = -2,       /* a HIP runtime call failed */
+    TFHE_AMD_E_NODEVICE = -3,  /* no usable GPU / the HIP kernels are not loadable */
+    TFHE_AMD_E_NOMEM = -4
+};
+
+/* gate codes (boot-gates.cu:98-448) */
+enum {
+    TFHE_GATE_NAND = 0, TFHE_GATE_OR = 1, TFHE_GATE_AND = 2, TFHE_GATE_XOR = 3,
+    TFHE_GATE_XNOR = 4, TFHE_GATE_NOR = 5, TFHE_GATE_ANDNY = 6, TFHE_GATE_ANDYN = 7,
+    TFHE_GATE_ORNY = 8, TFHE_GATE_ORYN = 9, TFHE_GATE_MUX = 10
+};
+
+typedef struct TfheAmdContext TfheAmdContext;
+
+/* Device context = the key material of one cloud key on one GPU: the NTT-domain
+ * bootstrapping key (converted on the device from the coefficient-domain key) and the
+ * key-switching key, plus a stream and scratch.  Replaces the reference's key upload
+ * (gpuParallel/main.cu:165-213 sendBootstrappingKeyToGPUCoalesceExt, :236-254, :364-407). */
+int tfhe_amd_context_create(const TFheGateBootstrappingCloudKeySet *bk, int device, TfheAmdContext **out);
+/* same from raw arrays: bk int32 [500][4][2][1024], ksk int32 [1024][8][4][501] */
+int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk, int device, TfheAmdContext **out);
+int tfhe_amd_context_destroy(TfheAmdContext *ctx);
+int tfhe_amd_context_device(const TfheAmdContext *ctx);
+/* the context's stream as a hipStream_t (void*) */
+void *tfhe_amd_context_stream(TfheAmdContext *ctx);
+int tfhe_amd_sync(TfheAmdContext *ctx);
+/* pre-size the scratch for batches of up to B gates (optional; grows on demand otherwise) */
+int tfhe_amd_reserve(TfheAmdContext *ctx, int B);
+
+/* B gates; cc_* only for TFHE_GATE_MUX (result = a ? b : c).  res may alias inputs. */
+int tfhe_amd_gate_batch_dev(TfheAmdContext *ctx, int gate, int B,
+                            int32_t *res_a, int32_t *res_b,
+                            const int32_t *ca_a, const int32_t *ca_b,
+                            const int32_t *cb_a, const int32_t *cb_b,
+                            const int32_t *cc_a, const int32_t *cc_b, void *stream);
+int tfhe_amd_gate_batch_host(TfheAmdContext *ctx, int gate, int B,
+                             int32_t *res_a, int32_t *res_b,
+                             const int32_t *ca_a, const int32_t *ca_b,
+                             const int32_t *cb_a, const int32_t *cb_b,
+                             const int32_t *cc_a, const int32_t *cc_b);
+
+/* tfhe_bootstrap_woKS_FFT over B inputs x (n=500) -> u (N=1024): u_a [B][1024], u_b [B] */
+int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *ctx, int B, int32_t mu,
+                                      const int32_t *x_a, const int32_t *x_b,
+                                      int32_t *u_a, int32_t *u_b, void *stream);
+/* tfhe_bootstrap_FFT over B inputs (woKS + key switch) */
+int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *ctx, int B, int32_t mu,
+                                 const int32_t *x_a, const int32_t *x_b,
+                                 int32_t *res_a, int32_t *res_b, void *stream);
+/* lweKeySwitch over B samples u (N=1024) -> res (n=500) */
+int tfhe_amd_keyswitch_batch_dev(TfheAmdContext *ctx, int B,
+                                 const int32_t *u_a, const int32_t *u_b,
+                                 int32_t *res_a, int32_t *res_b, void *stream);
+
+/* host-pointer (synchronous) versions of the three above */
+int tfhe_amd_bootstrap_woks_batch_host(TfheAmdContext *ctx, int B, int32_t mu,
+                                       const int32_t *x_a, const int32_t *x_b,
+                                       int32_t *u_a, int32_t *u_b);
+int tfhe_amd_bootstrap_batch_host(TfheAmdContext *ctx, int B, int32_t mu,
+                                  const int32_t *x_a, const int32_t *x_b,
+                                  int32_t *res_a, int32_t *res_b);
+int tfhe_amd_keyswitch_batch_host(TfheAmdContext *ctx, int B,
+                                  const int32_t *u_a, const int32_t *u_b,
+                                  int32_t *res_a, int32_t *res_b);
+
+/* Debug/parity entry: run `iters` CMux steps of the blind rotation (i = 0..iters-1,
+ * tfhe_MuxRotate_FFT, skipping bara_i == 0 like tfhe_blindRotate_FFT) on B explicit
+ * accumulators acc [B][2][1024] in place, with rotations bara [B][iters]. */
+int tfhe_amd_blind_rotate_dev(TfheAmdContext *ctx, int B, int iters, int32_t *acc,
+                              const int32_t *bara, void *stream);
+
+/* Timing of the engine's own kernels (HIP events on the stream they run on):
+ * enable=1 starts accumulating; read returns the summed ms and launch counts of the
+ * blind-rotation kernel and the key-switch kernel since enabling. */
+int tfhe_amd_profile_enable(TfheAmdContext *ctx, int enable);
+int tfhe_amd_profile_read(TfheAmdContext *ctx, double *br_ms, int *br_launches,
+                          double *ks_ms, int *ks_launches);
+
+/* Convenience: the same batch over LweSample arrays (Tier-1 structs) with the device
+ * context cached per cloud key. */
+int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
+                         const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk);
+
+/* Device selection for the Tier-1 (single-gate) API: the GPU used by the cached
+ * context of every cloud key (default 0). */
+int tfhe_amd_set_default_device(int device);
+
+/* Key material export (host): bk int32 [500][4][2][1024], ksk int32 [1024][8][4][501] */
+int tfhe_amd_export_bk(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out);
+int tfhe_amd_export_ksk(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out);
+/* LWE secret key (int32 [500]) of a secret keyset */
+int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
+/* TLWE secret key (int32 [1024]; k = 1), = the extracted LWE key of woKS outputs */
+int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
+
+/* build tag, e.g. "tfhe_amd gfx950 ntt2x30 br-v1" */
+const char *tfhe_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

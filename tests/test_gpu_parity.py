@@ -1,0 +1,120 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, Torus32 bit-exact
+(SURVEY.md §8(c) P1), plus decryption truth tables (P2)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import tfhe_amd as T
+
+pytestmark = pytest.mark.gpu
+
+N, n = 1024, 500
+TRUTH = {
+    "NAND": lambda x, y: 1 - (x & y), "OR": lambda x, y: x | y, "AND": lambda x, y: x & y,
+    "XOR": lambda x, y: x ^ y, "XNOR": lambda x, y: 1 - (x ^ y), "NOR": lambda x, y: 1 - (x | y),
+    "ANDNY": lambda x, y: (1 - x) & y, "ANDYN": lambda x, y: x & (1 - y),
+    "ORNY": lambda x, y: (1 - x) | y, "ORYN": lambda x, y: x | (1 - y),
+}
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+def test_blind_rotate_steps_match_oracle(ctx, okey, rng):
+    """A few CMux steps (rotation + decomposition + exact NTT product + CRT) on explicit
+    accumulators, including the rotation edge cases 0 (skip), 1, N-1, N, N+1, 2N-1, 2N."""
+    torch = _torch()
+    B, iters = 6, 8
+    acc0 = rng.integers(-2**31, 2**31, (B, 2, N), dtype=np.int64).astype(np.int32)
+    bara = rng.integers(0, 2049, (B, iters), dtype=np.int64).astype(np.int32)
+    bara[0] = [0, 1, 1023, 1024, 1025, 2047, 2048, 5]
+    bara[1] = 2048
+    bara[2, :4] = 0
+    d_acc = torch.from_numpy(acc0.copy()).cuda()
+    d_bara = torch.from_numpy(bara).cuda()
+    ctx.blind_rotate_dev(d_acc, d_bara, iters)
+    ctx.sync()
+    got = d_acc.cpu().numpy()
+    for b in range(B):
+        want = acc0[b].copy()
+        for i in range(iters):
+            if bara[b, i] != 0:
+                want = okey.mux_rotate(want, i, int(bara[b, i]))
+        assert np.array_equal(got[b], want), f"ciphertext {b}"
+
+
+@pytest.mark.parametrize("gate", list(TRUTH))
+def test_gate_batch_bit_exact(ctx, okey, keyset, rng, gate):
+    B = 16
+    x = rng.integers(0, 2, B)
+    y = rng.integers(0, 2, B)
+    a_a, a_b = keyset.encrypt(x, rng)
+    b_a, b_b = keyset.encrypt(y, rng)
+    r_a, r_b = ctx.gate_host(gate, a_a, a_b, b_a, b_b)
+    o_a, o_b = okey.gate_batch(gate, a_a, a_b, b_a, b_b)
+    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), TRUTH[gate](x, y))
+
+
+def test_mux_bit_exact(ctx, okey, keyset, rng):
+    B = 16
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    r_a, r_b = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+    o_a, o_b = okey.gate_batch("MUX", sa, sb, xa, xb, ya, yb)
+    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), np.where(s == 1, x, y))
+
+
+def test_woks_and_keyswitch_bit_exact(ctx, okey, keyset, rng):
+    B = 8
+    x_a = rng.integers(-2**31, 2**31, (B, n), dtype=np.int64).astype(np.int32)
+    x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    x_b[0] = np.int32(-2**20 + 5)      # modSwitch wrap edge: barb = 0
+    x_a[1, :50] = np.int32(-(2**20))   # bara = 0 through the wrap on a run of keys
+    x_a[2, :50] = 0                    # bara = 0 (skipped CMux)
+    u_a, u_b = ctx.woks_host(T.MU, x_a, x_b)
+    o_a, o_b = okey.woks_batch(T.MU, x_a, x_b)
+    assert np.array_equal(u_a, o_a) and np.array_equal(u_b, o_b)
+    k_a, k_b = ctx.keyswitch_host(u_a, u_b)
+    ko_a, ko_b = okey.keyswitch_batch(o_a, o_b)
+    assert np.array_equal(k_a, ko_a) and np.array_equal(k_b, ko_b)
+    r_a, r_b = ctx.bootstrap_host(T.MU, x_a, x_b)
+    assert np.array_equal(r_a, ko_a) and np.array_equal(r_b, ko_b)
+
+
+def test_keyswitch_random_inputs(ctx, okey, rng):
+    B = 5
+    u_a = rng.integers(-2**31, 2**31, (B, N), dtype=np.int64).astype(np.int32)
+    u_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    u_a[0] = 0                          # every digit of aibar = 2^15 is 0 except none
+    k_a, k_b = ctx.keyswitch_host(u_a, u_b)
+    o_a, o_b = okey.keyswitch_batch(u_a, u_b)
+    assert np.array_equal(k_a, o_a) and np.array_equal(k_b, o_b)
+
+
+def test_device_batch_1024_truth_and_sampled_parity(ctx, okey, keyset, rng):
+    """BASELINE config 2: 1024 independent bootsNAND on one GPU; every output decrypts to
+    the truth table, a sample of 32 is checked bit-exactly against the oracle."""
+    torch = _torch()
+    B = 1024
+    x = rng.integers(0, 2, B)
+    y = rng.integers(0, 2, B)
+    a_a, a_b = keyset.encrypt(x, rng)
+    b_a, b_b = keyset.encrypt(y, rng)
+    dev = [torch.from_numpy(v).cuda() for v in (a_a, a_b, b_a, b_b)]
+    r_a = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    r_b = torch.empty(B, dtype=torch.int32, device="cuda")
+    ctx.reserve(B)
+    ctx.gate_dev("NAND", r_a, r_b, *dev)
+    ctx.sync()
+    r_a, r_b = r_a.cpu().numpy(), r_b.cpu().numpy()
+    assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - (x & y))
+    idx = rng.choice(B, 32, replace=False)
+    o_a, o_b = okey.gate_batch("NAND", a_a[idx], a_b[idx], b_a[idx], b_b[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
