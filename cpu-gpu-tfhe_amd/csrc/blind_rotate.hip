@@ -1,0 +1,488 @@
+// blind_rotate.hip — v2 blind rotation for gfx950: register-resident exact NTTs.
+//
+// Same contract as bootstrap.hip's v1 (tfhe_blindRotate_FFT + extraction,
+// lwe-bootstrapping-functions-fft.cu:676-737, 1408-1456, 1834-1870; tGswFFTExternMulToTLwe
+// tgsw-fft-operations.cu:124-264), re-laid out for CDNA4:
+//
+//  * one 128-thread workgroup (2 waves) per ciphertext; wave s owns prime q_s.  It holds the
+//    4 digit polynomials of the decomposed accumulator (4 x 16 values per lane) through the
+//    forward NTT, the pointwise MAC with BK_i and the 2 inverse NTTs in VGPRs;
+//  * a 1024-point negacyclic NTT = 10 radix-2 stages in 3 register layouts
+//      A: lane L, reg r <-> j = L + 64 r          (stages 9..6, wave-uniform twiddles: SGPRs)
+//      B: j = (L & 3) | r << 2 | (L >> 2) << 6     (stages 5..2)
+//      C: j = 16 L + r                            (stages 1,0 fwd; 0..3 inv; MAC; BK loads)
+//    with two LDS transposes per transform through a per-wave padded scratch
+//    (word address j + 4 (j >> 6): conflict-free for b32 A/B and b128 C accesses);
+//  * Harvey lazy butterflies (values in [0, 4q) forward, [0, 2q) inverse) with Shoup
+//    twiddles; lane-varying twiddles come from "stream" tables laid out in consumption
+//    order (one coalesced 512-B load per slot);
+//  * the MAC reads BK_i (NTT domain, Montgomery form, 1/N folded) as 16-B loads from a
+//    lane-major layout, sums 4 rows in 64 bits and reduces once (REDC);
+//  * the two primes meet in a CRT exchange through LDS; the accumulator lives in LDS.
+#include "engine.h"
+#include "modarith.h"
+
+namespace tfhe_amd {
+
+namespace {
+
+constexpr int kV2Threads = 128;
+constexpr int kPadRow = kN + 64;   // padded scratch row: index j at word j + 4 (j >> 6)
+
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// 16-B LDS vector that may alias the uint32_t view of the same scratch (the transposes write
+// b32 and read b128 and vice versa: without may_alias, TBAA lets the compiler hoist the b128
+// reads above the b32 writes of the same wave)
+typedef uint32_t lds_u32x4 __attribute__((ext_vector_type(4), may_alias));
+
+// Cooley-Tukey (forward) butterfly, Harvey: x, y in [0, 4q) -> [0, 4q)
+__device__ __forceinline__ void bf_ct(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t q, uint32_t q2) {
+    const uint32_t u = umin32(x, x - q2);
+    const uint32_t t = y * w - __umulhi(y, wp) * q;   // [0, 2q)
+    x = u + t;
+    y = u - t + q2;
+}
+// Gentleman-Sande (inverse) butterfly, Harvey: x, y in [0, 2q) -> [0, 2q)
+__device__ __forceinline__ void bf_gs(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t q, uint32_t q2) {
+    const uint32_t s = x + y;
+    const uint32_t t = x - y + q2;
+    x = umin32(s, s - q2);
+    y = t * w - __umulhi(t, wp) * q;
+}
+
+// Lanes of one wave exchange values through LDS in the transposes.  Single-thread
+// semantics let the compiler hoist a lane's read above another lane's write whenever it
+// can prove the two addresses differ FOR THE SAME LANE (it did, e.g. load_B(r < 8) above
+// the last store_A: every coefficient came out wrong).  A wavefront-scope release/acquire
+// pair around a wave barrier pins the order; LDS itself executes one wave's DS
+// instructions in order.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- layout transposes through the per-wave scratch (one polynomial)
+__device__ __forceinline__ void store_A(uint32_t *sc, const uint32_t (&x)[16], int L) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[L + 68 * r] = x[r];            // j = L + 64 r
+}
+__device__ __forceinline__ void load_A(const uint32_t *sc, uint32_t (&x)[16], int L) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = sc[L + 68 * r];
+}
+__device__ __forceinline__ int base_B(int L) { return (L & 3) + 68 * (L >> 2); }
+__device__ __forceinline__ void store_B(uint32_t *sc, const uint32_t (&x)[16], int L) {
+    uint32_t *p = sc + base_B(L);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p[4 * r] = x[r];                   // j = (L&3) | r<<2 | (L>>2)<<6
+}
+__device__ __forceinline__ void load_B(const uint32_t *sc, uint32_t (&x)[16], int L) {
+    const uint32_t *p = sc + base_B(L);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = p[4 * r];
+}
+__device__ __forceinline__ int base_C(int L) { return 16 * L + 4 * (L >> 2); }
+__device__ __forceinline__ void store_C(uint32_t *sc, const uint32_t (&x)[16], int L) {
+    lds_u32x4 *p = reinterpret_cast<lds_u32x4 *>(sc + base_C(L));    // j = 16 L + r
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        lds_u32x4 t;
+        t.x = x[4 * v]; t.y = x[4 * v + 1]; t.z = x[4 * v + 2]; t.w = x[4 * v + 3];
+        p[v] = t;
+    }
+}
+__device__ __forceinline__ void load_C(const uint32_t *sc, uint32_t (&x)[16], int L) {
+    const lds_u32x4 *p = reinterpret_cast<const lds_u32x4 *>(sc + base_C(L));
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const lds_u32x4 t = p[v];
+        x[4 * v] = t.x; x[4 * v + 1] = t.y; x[4 * v + 2] = t.z; x[4 * v + 3] = t.w;
+    }
+}
+
+// ---- forward NTT of NP polys (layout A in, layout C out), values [0,4q)
+template <int NP>
+__device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
+                                        const uint2 *__restrict__ ts, int L, uint32_t q) {
+    const uint32_t q2 = 2 * q;
+#pragma unroll
+    for (int K = 9; K >= 6; --K) {                     // layout A, uniform twiddles
+        const int d = 1 << (K - 6);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_A(sc, x[p], L);
+        wave_lds_sync();
+        load_B(sc, x[p], L);
+        wave_lds_sync();
+    }
+    int slot = 0;
+#pragma unroll
+    for (int K = 5; K >= 2; --K) {                     // layout B, per-lane twiddles
+        const int d = 1 << (K - 2), cnt = 1 << (5 - K);
+        uint2 tw[8];
+#pragma unroll
+        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
+        slot += cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tw[r >> (K - 1)];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_B(sc, x[p], L);
+        wave_lds_sync();
+        load_C(sc, x[p], L);
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int K = 1; K >= 0; --K) {                     // layout C
+        const int d = 1 << K, cnt = 1 << (3 - K);
+        uint2 tw[8];
+#pragma unroll
+        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
+        slot += cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tw[r >> (K + 1)];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+}
+
+// ---- inverse NTT of NP polys (layout C in, layout A out), values [0,2q) -> [0,2q)
+template <int NP>
+__device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
+                                        const uint2 *__restrict__ ts, int L, uint32_t q) {
+    const uint32_t q2 = 2 * q;
+    int slot = 0;
+#pragma unroll
+    for (int K = 0; K <= 3; ++K) {                     // layout C
+        const int d = 1 << K, cnt = 1 << (3 - K);
+        uint2 tw[8];
+#pragma unroll
+        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
+        slot += cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tw[r >> (K + 1)];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_C(sc, x[p], L);
+        wave_lds_sync();
+        load_B(sc, x[p], L);
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int K = 4; K <= 5; ++K) {                     // layout B
+        const int d = 1 << (K - 2), cnt = 1 << (5 - K);
+        uint2 tw[2];
+#pragma unroll
+        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
+        slot += cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tw[r >> (K - 1)];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_B(sc, x[p], L);
+        wave_lds_sync();
+        load_A(sc, x[p], L);
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int K = 6; K <= 9; ++K) {                     // layout A, uniform twiddles
+        const int d = 1 << (K - 6);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (r & d) continue;
+            const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+        }
+    }
+}
+
+struct V2Shared {
+    uint32_t acc[2][kN];               // TLWE accumulator (a, b)
+    uint32_t scratch[2][kPadRow];      // one per wave (prime)
+    int bara[512];
+    int barb;
+};
+
+struct V2Args {
+    const uint32_t *bk;   // [kn][2][2 c][4 p][4 v][64 L][4 e]   (Montgomery, 1/N folded)
+    const uint2 *tu_f;    // [2][16] uniform forward twiddles (idx 1..15)
+    const uint2 *tu_i;    // [2][16]
+    const uint2 *ts_f;    // [2][27][64] stream forward twiddles
+    const uint2 *ts_i;    // [2][18][64]
+    uint32_t qinv_neg0, qinv_neg1, crt_h, crt_hp;
+};
+
+// CRT exchange + accumulate; wave S handles r in [8S, 8S+8) of both polys.  Split in a
+// give (write) and a take (read + accumulate) half so that the workgroup barrier between
+// them sits in uniform control flow (a barrier inside the per-wave `if (s == 0)` branches
+// was miscompiled: results wrong on every coefficient).
+template <int S>
+__device__ __forceinline__ void crt_give(V2Shared &sh, const uint32_t (&O)[2][16], int L) {
+    uint32_t *mine = sh.scratch[S];
+    constexpr int give = 8 * (1 - S);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) mine[(c * 8 + rr) * 64 + L] = O[c][give + rr];
+}
+template <int S>
+__device__ __forceinline__ void crt_take(V2Shared &sh, const uint32_t (&O)[2][16], int L, const V2Args &g) {
+    const uint32_t *other = sh.scratch[1 - S];
+    constexpr int keep = 8 * S;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+            const uint32_t xo = other[(c * 8 + rr) * 64 + L];
+            const uint32_t xm = O[c][keep + rr];
+            const uint32_t x0 = S == 0 ? xm : xo, x1 = S == 0 ? xo : xm;
+            sh.acc[c][L + 64 * (keep + rr)] += crt_torus(x0, x1, g.crt_h, g.crt_hp);
+        }
+}
+
+// one CMux step for key index i and rotation a (1..2N-1); called by both waves
+__device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, int a, int s, int L) {
+    const uint32_t q = s ? kQ1 : kQ0;
+    const uint32_t q2 = 2 * q;
+    uint32_t *sc = sh.scratch[s];
+    // (X^a - 1) ACC + gadget decomposition, layout A; digits lifted to [q-512, q+511]
+    uint32_t D[4][16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int j = L + 64 * r;
+            const int si = (j - a) & (k2N - 1);
+            const uint32_t v = sh.acc[c][si & (kN - 1)];
+            const uint32_t rot = (si & kN) ? 0u - v : v;
+            const uint32_t t = rot - sh.acc[c][j] + kDecompOffset;
+            D[2 * c][r] = ((t >> 22) & 1023u) + (q - 512u);
+            D[2 * c + 1][r] = ((t >> 12) & 1023u) + (q - 512u);
+        }
+    ntt_fwd<4>(D, sc, g.tu_f + 16 * s, g.ts_f + s * 27 * 64 + L, L, q);
+    // pointwise MAC with BK_i (layout C: reg r = 4 v + e <-> j = 16 L + r)
+    const uint4 *bk4 = reinterpret_cast<const uint4 *>(g.bk + ((size_t)(i * 2 + s) * 8) * kN) + L;
+    const uint32_t qinv = s ? g.qinv_neg1 : g.qinv_neg0;
+    uint32_t O[2][16];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) D[p][4 * v + e] = umin32(D[p][4 * v + e], D[p][4 * v + e] - q2);   // [0,2q)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uint4 b[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) b[p] = bk4[(c * 4 + p) * 256 + v * 64];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t b0 = e == 0 ? b[0].x : e == 1 ? b[0].y : e == 2 ? b[0].z : b[0].w;
+                const uint32_t b1 = e == 0 ? b[1].x : e == 1 ? b[1].y : e == 2 ? b[1].z : b[1].w;
+                const uint32_t b2 = e == 0 ? b[2].x : e == 1 ? b[2].y : e == 2 ? b[2].z : b[2].w;
+                const uint32_t b3 = e == 0 ? b[3].x : e == 1 ? b[3].y : e == 2 ? b[3].z : b[3].w;
+                const int r = 4 * v + e;
+                const uint64_t x = (uint64_t)D[0][r] * b0 + (uint64_t)D[1][r] * b1 + (uint64_t)D[2][r] * b2 +
+                                   (uint64_t)D[3][r] * b3;                          // < 8 q^2
+                const uint32_t m = (uint32_t)x * qinv;
+                const uint32_t t = (uint32_t)((x + (uint64_t)m * q) >> 32);    // < 3q
+                O[c][r] = umin32(t, t - q2);                                     // [0, 2q)
+            }
+        }
+    }
+    ntt_inv<2>(O, sc, g.tu_i + 16 * s, g.ts_i + s * 18 * 64 + L, L, q);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[c][r] = umin32(O[c][r], O[c][r] - q);   // [0, q)
+    if (s == 0) crt_give<0>(sh, O, L);
+    else crt_give<1>(sh, O, L);
+    __syncthreads();
+    if (s == 0) crt_take<0>(sh, O, L, g);
+    else crt_take<1>(sh, O, L, g);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kV2Threads) void k_blind_rotate_v2(V2Args g, int B, BrInput in0, BrInput in1,
+                                                                int32_t mu, int32_t *__restrict__ u_a,
+                                                                int32_t *__restrict__ u_b) {
+    __shared__ V2Shared sh;
+    const int tid = threadIdx.x;
+    const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    const int gct = blockIdx.x;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+
+    // gate prologue + modulus switching (boot-gates.cu:98-397; lwe-bootstrapping-functions-fft.cu:1851-1858)
+    for (int i = tid; i < kn; i += kV2Threads) {
+        uint32_t x = (uint32_t)in.sa * (uint32_t)in.x_a[(size_t)idx * kn + i];
+        if (in.sb) x += (uint32_t)in.sb * (uint32_t)in.y_a[(size_t)idx * kn + i];
+        sh.bara[i] = modswitch_2N(x);
+    }
+    if (tid == 0) {
+        uint32_t xb = (uint32_t)in.c + (uint32_t)in.sa * (uint32_t)in.x_b[idx];
+        if (in.sb) xb += (uint32_t)in.sb * (uint32_t)in.y_b[idx];
+        sh.barb = modswitch_2N(xb);
+    }
+    __syncthreads();
+    {   // ACC = (0, X^{2N - barb} (mu, ..., mu))   (:1427-1431)
+        const int e = (k2N - sh.barb) & (k2N - 1);
+        for (int j = tid; j < kN; j += kV2Threads) {
+            sh.acc[0][j] = 0;
+            const int si = (j - e) & (k2N - 1);
+            sh.acc[1][j] = si < kN ? (uint32_t)mu : 0u - (uint32_t)mu;
+        }
+    }
+    __syncthreads();
+    for (int i = 0; i < kn; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
+        cmux_v2(sh, g, i, a, s, L);
+    }
+    // sample extraction at index 0 (lwe.cu:41-56)
+    int32_t *ua = u_a + (size_t)gct * kN;
+    for (int j = tid; j < kN; j += kV2Threads)
+        ua[j] = (int32_t)(j == 0 ? sh.acc[0][0] : 0u - sh.acc[0][kN - j]);
+    if (tid == 0) u_b[gct] = (int32_t)sh.acc[1][0];
+}
+
+__global__ __launch_bounds__(kV2Threads) void k_blind_rotate_v2_debug(V2Args g, int iters, int32_t *__restrict__ acc,
+                                                                      const int32_t *__restrict__ bara) {
+    __shared__ V2Shared sh;
+    const int tid = threadIdx.x;
+    const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
+    for (int j = tid; j < 2 * kN; j += kV2Threads) sh.acc[j >> kLogN][j & (kN - 1)] = (uint32_t)accg[j];
+    for (int i = tid; i < iters; i += kV2Threads) sh.bara[i] = bara[(size_t)blockIdx.x * iters + i] & (k2N - 1);
+    __syncthreads();
+    for (int i = 0; i < iters; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;
+        cmux_v2(sh, g, i, a, s, L);
+    }
+    for (int j = tid; j < 2 * kN; j += kV2Threads) accg[j] = (int32_t)sh.acc[j >> kLogN][j & (kN - 1)];
+}
+
+// BK (coefficient domain [i][p][c][N]) -> v2 layout [i][s][c][p][v][L][e], j = 16 L + 4 v + e,
+// from the v1 NTT-domain key [i][s][p][c][N] (same values, bit-reversed NTT order j)
+__global__ __launch_bounds__(256) void k_bk_v1_to_v2(const uint32_t *__restrict__ v1, uint32_t *__restrict__ v2) {
+    const int poly = blockIdx.x;   // (i*2 + s)*8 + c*4 + p
+    const int p = poly & 3, c = (poly >> 2) & 1, is = poly >> 3;
+    const uint32_t *src = v1 + ((size_t)is * 8 + p * 2 + c) * kN;
+    uint32_t *dst = v2 + (size_t)poly * kN;
+    for (int j = threadIdx.x; j < kN; j += blockDim.x) {
+        const int L = j >> 4, v = (j >> 2) & 3, e = j & 3;
+        dst[v * 256 + L * 4 + e] = src[j];
+    }
+}
+
+}  // namespace
+
+// Twiddle tables of the v2 kernel, generated on the host in the kernel's consumption order.
+void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f, uint2 *ts_i) {
+    for (int s = 0; s < 2; ++s) {
+        for (int idx = 0; idx < 16; ++idx) {
+            tu_f[s * 16 + idx] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+            tu_i[s * 16 + idx] = make_uint2(t.ipsi[s][idx], t.ipsip[s][idx]);
+        }
+        int slot = 0;
+        for (int K = 5; K >= 2; --K)
+            for (int g = 0; g < (1 << (5 - K)); ++g, ++slot)
+                for (int L = 0; L < 64; ++L) {
+                    const int idx = (1 << (9 - K)) + ((L >> 2) << (5 - K)) + g;
+                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+                }
+        for (int K = 1; K >= 0; --K)
+            for (int g = 0; g < (1 << (3 - K)); ++g, ++slot)
+                for (int L = 0; L < 64; ++L) {
+                    const int idx = (1 << (9 - K)) + (L << (3 - K)) + g;
+                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+                }
+        slot = 0;
+        for (int K = 0; K <= 3; ++K)
+            for (int g = 0; g < (1 << (3 - K)); ++g, ++slot)
+                for (int L = 0; L < 64; ++L) {
+                    const int idx = (1 << (9 - K)) + (L << (3 - K)) + g;
+                    ts_i[(s * 18 + slot) * 64 + L] = make_uint2(t.ipsi[s][idx], t.ipsip[s][idx]);
+                }
+        for (int K = 4; K <= 5; ++K)
+            for (int g = 0; g < (1 << (5 - K)); ++g, ++slot)
+                for (int L = 0; L < 64; ++L) {
+                    const int idx = (1 << (9 - K)) + ((L >> 2) << (5 - K)) + g;
+                    ts_i[(s * 18 + slot) * 64 + L] = make_uint2(t.ipsi[s][idx], t.ipsip[s][idx]);
+                }
+    }
+}
+
+static V2Args v2_args(const DeviceKey &key) {
+    V2Args g;
+    g.bk = key.bk_v2;
+    g.tu_f = key.tw2;
+    g.tu_i = key.tw2 + 32;
+    g.ts_f = key.tw2 + 64;
+    g.ts_i = key.tw2 + 64 + 2 * 27 * 64;
+    g.qinv_neg0 = key.qinv_neg[0];
+    g.qinv_neg1 = key.qinv_neg[1];
+    g.crt_h = key.crt_h;
+    g.crt_hp = key.crt_hp;
+    return g;
+}
+
+hipError_t launch_bk_v1_to_v2(const uint32_t *d_v1, uint32_t *d_v2, hipStream_t s) {
+    hipLaunchKernelGGL(k_bk_v1_to_v2, dim3(kn * 2 * 8), dim3(256), 0, s, d_v1, d_v2);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v2(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    const BrInput in1 = halves > 1 ? in[1] : in[0];
+    hipLaunchKernelGGL(k_blind_rotate_v2, dim3(B * halves), dim3(kV2Threads), 0, s, v2_args(key), B, in[0], in1, mu,
+                       u_a, u_b);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v2_debug(const DeviceKey &key, int B, int iters, int32_t *acc, const int32_t *bara,
+                                        hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (iters < 0 || iters > kn) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_v2_debug, dim3(B), dim3(kV2Threads), 0, s, v2_args(key), iters, acc, bara);
+    return hipGetLastError();
+}
+
+}  // namespace tfhe_amd

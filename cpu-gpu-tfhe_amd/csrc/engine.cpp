@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -67,6 +68,24 @@ void build_ntt_tables(NttTables *t) {
     t->crt_hp = shoup(t->crt_h, kQ[1]);
 }
 
+static std::atomic<int> g_br_version{0};
+
+int br_version() {
+    int v = g_br_version.load(std::memory_order_relaxed);
+    if (v == 0) {
+        const char *e = getenv("TFHE_AMD_BR");
+        v = (e && atoi(e) == 1) ? 1 : 2;
+        g_br_version.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
+static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
+                         int32_t *u_b, hipStream_t s) {
+    return br_version() == 1 ? launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s)
+                             : launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
+}
+
 }  // namespace tfhe_amd
 
 using namespace tfhe_amd;
@@ -107,6 +126,8 @@ struct TfheAmdContext {
 static int free_key(DeviceKey &k) {
     if (k.device >= 0) (void)hipSetDevice(k.device);
     if (k.bk_ntt) (void)hipFree(k.bk_ntt);
+    if (k.bk_v2) (void)hipFree(k.bk_v2);
+    if (k.tw2) (void)hipFree(k.tw2);
     if (k.ksk) (void)hipFree(k.ksk);
     if (k.tables) (void)hipFree(k.tables);
     k = DeviceKey();
@@ -155,6 +176,16 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
     build_ntt_tables(ht);
     HIPCHK(hipMalloc(&c->key.tables, sizeof(NttTables)));
     HIPCHK(hipMemcpy(c->key.tables, ht, sizeof(NttTables), hipMemcpyHostToDevice));
+    c->key.qinv_neg[0] = ht->qinv_neg[0];
+    c->key.qinv_neg[1] = ht->qinv_neg[1];
+    c->key.crt_h = ht->crt_h;
+    c->key.crt_hp = ht->crt_hp;
+    {
+        std::vector<uint2> tw(kTw2Words);
+        build_v2_twiddles(*ht, tw.data(), tw.data() + 32, tw.data() + 64, tw.data() + 64 + 2 * 27 * 64);
+        HIPCHK(hipMalloc(&c->key.tw2, sizeof(uint2) * tw.size()));
+        HIPCHK(hipMemcpy(c->key.tw2, tw.data(), sizeof(uint2) * tw.size(), hipMemcpyHostToDevice));
+    }
     delete ht;
 
     if (bk) {
@@ -164,6 +195,8 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         HIPCHK(hipMemcpy(d_coef, bk, sizeof(int32_t) * coef_words, hipMemcpyHostToDevice));
         HIPCHK(hipMalloc(&c->key.bk_ntt, sizeof(uint32_t) * 2 * coef_words));
         HIPCHK(launch_bk_to_ntt(d_coef, c->key.bk_ntt, c->key.tables, c->stream));
+        HIPCHK(hipMalloc(&c->key.bk_v2, sizeof(uint32_t) * 2 * coef_words));
+        HIPCHK(launch_bk_v1_to_v2(c->key.bk_ntt, c->key.bk_v2, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(d_coef));
         c->key.has_bk = true;
@@ -321,7 +354,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
         BrInput in[2] = {{ca_a, ca_b, cb_a, cb_b, -kMu, 1, 1}, {ca_a, ca_b, cc_a, cc_b, -kMu, -1, 1}};
         {
             ProfScope ps(c, s, true);
-            HIPCHK(launch_blind_rotate(c->key, B, 2, in, kMu, c->u_a, c->u_b, s));
+            HIPCHK(run_br(c->key, B, 2, in, kMu, c->u_a, c->u_b, s));
         }
         ProfScope ps(c, s, false);
         HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, c->u_a + (size_t)B * kN, c->u_b + B, kMu,
@@ -333,7 +366,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     in.x_a = ca_a; in.x_b = ca_b; in.y_a = cb_a; in.y_b = cb_b;
     {
         ProfScope ps(c, s, true);
-        HIPCHK(launch_blind_rotate(c->key, B, 1, &in, kMu, c->u_a, c->u_b, s));
+        HIPCHK(run_br(c->key, B, 1, &in, kMu, c->u_a, c->u_b, s));
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
@@ -349,7 +382,7 @@ extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32
     HIPCHK(hipSetDevice(c->device));
     BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
     ProfScope ps(c, s, true);
-    HIPCHK(launch_blind_rotate(c->key, B, 1, &in, mu, u_a, u_b, s));
+    HIPCHK(run_br(c->key, B, 1, &in, mu, u_a, u_b, s));
     return TFHE_AMD_OK;
 }
 
@@ -365,7 +398,7 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
     {
         ProfScope ps(c, s, true);
-        HIPCHK(launch_blind_rotate(c->key, B, 1, &in, mu, c->u_a, c->u_b, s));
+        HIPCHK(run_br(c->key, B, 1, &in, mu, c->u_a, c->u_b, s));
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
@@ -392,7 +425,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, s, true);
-    HIPCHK(launch_blind_rotate_debug(c->key, B, iters, acc, bara, s));
+    HIPCHK(br_version() == 1 ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
+                             : launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
 
@@ -494,4 +528,12 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
     return c;
 }
 
-extern "C" const char *tfhe_amd_version(void) { return "tfhe_amd gfx950 ntt2x30 br-v1 ks-v1"; }
+extern "C" int tfhe_amd_select_kernel(int br_version) {
+    if (br_version != 1 && br_version != 2) return TFHE_AMD_E_ARG;
+    g_br_version.store(br_version);
+    return TFHE_AMD_OK;
+}
+
+extern "C" const char *tfhe_amd_version(void) {
+    return br_version() == 1 ? "tfhe_amd gfx950 ntt2x30 br-v1 ks-v1" : "tfhe_amd gfx950 ntt2x30 br-v2 ks-v1";
+}

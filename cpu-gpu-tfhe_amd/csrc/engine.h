@@ -10,11 +10,16 @@ namespace tfhe_amd {
 // Key material of one cloud key resident on one GPU.
 struct DeviceKey {
     int device = -1;
-    uint32_t *bk_ntt = nullptr;   // [kn][2 primes][kKpl][2][kN], Montgomery form, 1/N folded
+    uint32_t *bk_ntt = nullptr;   // v1: [kn][2 primes][kKpl][2][kN], Montgomery form, 1/N folded
+    uint32_t *bk_v2 = nullptr;    // v2: [kn][2 primes][2 c][kKpl][4 v][64 L][4 e] (same values)
+    uint2 *tw2 = nullptr;         // v2 twiddles: uniform fwd/inv [2][16] x2, streams [2][27][64], [2][18][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     NttTables *tables = nullptr;  // device copy
+    uint32_t qinv_neg[2] = {0, 0};
+    uint32_t crt_h = 0, crt_hp = 0;
     bool has_bk = false;
 };
+constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -33,6 +38,16 @@ hipError_t launch_blind_rotate(const DeviceKey &key, int B, int halves, const Br
 // Debug: `iters` CMux steps on explicit accumulators acc [B][2][kN] with bara [B][iters].
 hipError_t launch_blind_rotate_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                      const int32_t *bara, hipStream_t s);
+// v2 (register-resident NTT) variants, blind_rotate.hip
+void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f, uint2 *ts_i);
+hipError_t launch_bk_v1_to_v2(const uint32_t *d_v1, uint32_t *d_v2, hipStream_t s);
+hipError_t launch_blind_rotate_v2(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v2_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                        const int32_t *bara, hipStream_t s);
+// which blind-rotation kernel runs: 2 (default) or 1 (env TFHE_AMD_BR=1)
+int br_version();
+
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).
 hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,
                             const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,

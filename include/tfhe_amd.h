@@ -124,6 +124,11 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 /* TLWE secret key (int32 [1024]; k = 1), = the extracted LWE key of woKS outputs */
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
+/* Select the blind-rotation kernel generation (1 = LDS radix-2 reference kernel,
+ * 2 = register-resident NTT, the default; env TFHE_AMD_BR=1 does the same at startup).
+ * For A/B measurements and parity cross-checks; results are identical by contract. */
+int tfhe_amd_select_kernel(int br_version);
+
 /* build tag, e.g. "tfhe_amd gfx950 ntt2x30 br-v1" */
 const char *tfhe_amd_version(void);
 

@@ -19,4 +19,5 @@ done
 g++ -std=c++11 -O2 -fPIC -fwrapv -c "$HERE/ref_driver.cpp" -I"$REF" -o "$OUT/ref_driver.o"
 g++ -shared -o "$OUT/libtfheref.so" $OBJS "$OUT/ref_driver.o"
 rm -f $OBJS "$OUT/ref_driver.o"
+g++ -std=c++11 -Wno-invalid-offsetof -I"$REF" "$HERE/ref_layout.cpp" -o "$OUT/ref_layout"
 echo "built $OUT/libtfheref.so"

@@ -112,6 +112,13 @@ def main():
     out["lweop_out_a"] = oa
     out["lweop_out_b"] = ob
 
+    # (5) struct layouts of the reference's own headers (oracle/ref_layout.cpp)
+    import json
+    import subprocess
+    lay = subprocess.check_output([os.path.join(REPO, "oracle", "_ref", "ref_layout")]).decode()
+    with open(os.path.join(HERE, "abi_layout.json"), "w") as f:
+        json.dump(json.loads(lay), f, indent=1, sort_keys=True)
+
     path = os.path.join(HERE, "ref_leaf_vectors.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")
