@@ -13,7 +13,7 @@
 //      C: j = 16 L + r                            (stages 1,0 fwd; 0..3 inv; MAC; BK loads)
 //    with two LDS transposes per transform through a per-wave padded scratch
 //    (word address j + 4 (j >> 6): conflict-free for b32 A/B and b128 C accesses);
-//  * Harvey lazy butterflies (values in [0, 4q) forward, [0, 2q) inverse) with Shoup
+//  * lazy butterflies (forward: no reductions, values < 22q since q < 2^27; inverse: Harvey [0, 2q)), Shoup
 //    twiddles; lane-varying twiddles come from "stream" tables laid out in consumption
 //    order (one coalesced 512-B load per slot);
 //  * the MAC reads BK_i (NTT domain, Montgomery form, 1/N folded) as 16-B loads from a
@@ -36,19 +36,28 @@ __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < 
 // reads above the b32 writes of the same wave)
 typedef uint32_t lds_u32x4 __attribute__((ext_vector_type(4), may_alias));
 
-// Cooley-Tukey (forward) butterfly, Harvey: x, y in [0, 4q) -> [0, 4q)
-__device__ __forceinline__ void bf_ct(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t q, uint32_t q2) {
-    const uint32_t u = umin32(x, x - q2);
-    const uint32_t t = y * w - __umulhi(y, wp) * q;   // [0, 2q)
+// Shoup product y * w mod q, lazy: [0, 2q) for any y < 2^32.  y*w - qh*q (mod 2^32) is
+// folded into one v_mad_u64_u32: qh * (2^32 - q) + lo(y*w).
+__device__ __forceinline__ uint32_t shoup_lazy(uint32_t y, uint32_t w, uint32_t wp, uint32_t negq) {
+    const uint32_t qh = __umulhi(y, wp);
+    return (uint32_t)((uint64_t)qh * negq + (uint32_t)(y * w));
+}
+// Cooley-Tukey (forward) butterfly WITHOUT reductions: inputs < B -> outputs < B + 2q.
+// Digits enter < 2q, so after the 10 stages every value is < 22q < 2^32 (q < 2^27).
+__device__ __forceinline__ void bf_ct(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t negq,
+                                      uint32_t q2) {
+    const uint32_t t = shoup_lazy(y, w, wp, negq);    // [0, 2q)
+    const uint32_t u = x;
     x = u + t;
     y = u - t + q2;
 }
 // Gentleman-Sande (inverse) butterfly, Harvey: x, y in [0, 2q) -> [0, 2q)
-__device__ __forceinline__ void bf_gs(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t q, uint32_t q2) {
+__device__ __forceinline__ void bf_gs(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t negq,
+                                      uint32_t q2) {
     const uint32_t s = x + y;
     const uint32_t t = x - y + q2;
     x = umin32(s, s - q2);
-    y = t * w - __umulhi(t, wp) * q;
+    y = shoup_lazy(t, w, wp, negq);
 }
 
 // Lanes of one wave exchange values through LDS in the transposes.  Single-thread
@@ -102,11 +111,11 @@ __device__ __forceinline__ void load_C(const uint32_t *sc, uint32_t (&x)[16], in
     }
 }
 
-// ---- forward NTT of NP polys (layout A in, layout C out), values [0,4q)
+// ---- forward NTT of NP polys (layout A in, layout C out), values < 2q in, < 22q out
 template <int NP>
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
                                         const uint2 *__restrict__ ts, int L, uint32_t q) {
-    const uint32_t q2 = 2 * q;
+    const uint32_t q2 = 2 * q, negq = 0u - q;
 #pragma unroll
     for (int K = 9; K >= 6; --K) {                     // layout A, uniform twiddles
         const int d = 1 << (K - 6);
@@ -115,7 +124,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 #pragma unroll
@@ -138,7 +147,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tw[r >> (K - 1)];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 #pragma unroll
@@ -160,7 +169,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tw[r >> (K + 1)];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 }
@@ -169,7 +178,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
 template <int NP>
 __device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
                                         const uint2 *__restrict__ ts, int L, uint32_t q) {
-    const uint32_t q2 = 2 * q;
+    const uint32_t q2 = 2 * q, negq = 0u - q;
     int slot = 0;
 #pragma unroll
     for (int K = 0; K <= 3; ++K) {                     // layout C
@@ -183,7 +192,7 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tw[r >> (K + 1)];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 #pragma unroll
@@ -205,7 +214,7 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tw[r >> (K - 1)];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 #pragma unroll
@@ -223,7 +232,7 @@ __device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, con
             if (r & d) continue;
             const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, q, q2);
+            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
         }
     }
 }
@@ -299,10 +308,6 @@ __device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, in
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int p = 0; p < 4; ++p) D[p][4 * v + e] = umin32(D[p][4 * v + e], D[p][4 * v + e] - q2);   // [0,2q)
-#pragma unroll
         for (int c = 0; c < 2; ++c) {
             uint4 b[4];
 #pragma unroll
@@ -315,9 +320,9 @@ __device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, in
                 const uint32_t b3 = e == 0 ? b[3].x : e == 1 ? b[3].y : e == 2 ? b[3].z : b[3].w;
                 const int r = 4 * v + e;
                 const uint64_t x = (uint64_t)D[0][r] * b0 + (uint64_t)D[1][r] * b1 + (uint64_t)D[2][r] * b2 +
-                                   (uint64_t)D[3][r] * b3;                          // < 8 q^2
+                                   (uint64_t)D[3][r] * b3;                          // < 88 q^2 < 2^61
                 const uint32_t m = (uint32_t)x * qinv;
-                const uint32_t t = (uint32_t)((x + (uint64_t)m * q) >> 32);    // < 3q
+                const uint32_t t = (uint32_t)((x + (uint64_t)m * q) >> 32);    // < 3.75 q
                 O[c][r] = umin32(t, t - q2);                                     // [0, 2q)
             }
         }

@@ -7,8 +7,8 @@
 
 namespace tfhe_amd {
 
-constexpr uint32_t kQ0 = 1073707009u;
-constexpr uint32_t kQ1 = 1073698817u;
+constexpr uint32_t kQ0 = 134215681u;
+constexpr uint32_t kQ1 = 134203393u;
 static_assert(kQ0 == kQ[0] && kQ1 == kQ[1], "prime mismatch");
 
 __device__ __forceinline__ uint32_t q_of(int s) { return s ? kQ1 : kQ0; }

@@ -24,9 +24,11 @@ constexpr uint32_t kKsPrecOffset = 1u << (32 - (1 + kKsBasebit * kKsT)); // 2^15
 // each row = 500 a-coefficients, b, zero padding to 512 int32 (2 KB, 16-B aligned).
 constexpr int kKsRow = 512;
 
-// The exact external product: 2-prime CRT NTT, q < 2^30, q == 1 mod 2N.
-// q0*q1 ~ 2^60 > 2 * (4 rows * 1024 * 512 * 2^31) = 2^53 (SURVEY.md §7.3 option (i)).
-constexpr uint32_t kQ[2] = {1073707009u, 1073698817u};
+// The exact external product: 2-prime CRT NTT, q < 2^27, q == 1 mod 2N (the two largest
+// such primes).  q0*q1 = 1.99976 * 2^53 > 2 * (4 rows * 1024 * 512 * 2^31) = 2^53, so the
+// centred CRT lift is exact (SURVEY.md §7.3 option (i)).  q < 2^27 leaves 32q of headroom
+// in 32-bit lanes: the lazy forward NTT needs no reductions at all (values stay < 22q).
+constexpr uint32_t kQ[2] = {134215681u, 134203393u};
 
 // standard deviations, tfhe_gate_bootstrapping.cu:36-38 (mulBySqrtTwoOverPi :22)
 constexpr double kKsStdev = 2.4349504419032758e-05;   // sqrt(2/pi) * 2^-15

@@ -5,7 +5,7 @@ import os
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests'))
 import oracle_ctypes as O
 N=1024
-Q=[1073707009,1073698817]
+Q=[134215681,134203393]
 M32=0xFFFFFFFF
 def powmod(b,e,q): return pow(b,e,q)
 def brv(x,b=10): return int('{:0{w}b}'.format(x,w=b)[::-1],2)
@@ -39,8 +39,9 @@ def streams(s):
 def umin(a,b): return a if a<b else b
 def bf_ct(x,y,w,wp,q):
     q2=2*q
-    u=umin(x,(x-q2)&M32)
+    u=x
     t=(y*w - ((y*wp)>>32)*q)&M32
+    assert u+t < 2**32 and u+q2 < 2**32
     return (u+t)&M32, (u-t+q2)&M32
 def bf_gs(x,y,w,wp,q):
     q2=2*q
@@ -185,7 +186,7 @@ def _selftest():
             O=[[[0]*16 for _ in range(64)] for _ in range(2)]
             for L in range(64):
                 for r in range(16):
-                    dd=[umin(D[p][L][r],(D[p][L][r]-2*q)&M32) for p in range(4)]
+                    dd=[D[p][L][r] for p in range(4)]
                     j=16*L+r
                     for c in range(2):
                         x=sum(dd[p]*bkntt[(s,p,c)][j] for p in range(4))
