@@ -74,7 +74,8 @@ int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
     if (v == 0) {
         const char *e = getenv("TFHE_AMD_BR");
-        v = (e && atoi(e) == 1) ? 1 : 2;
+        v = e ? atoi(e) : 2;
+        if (v < 1 || v > 3) v = 2;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
@@ -82,8 +83,11 @@ int br_version() {
 
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
                          int32_t *u_b, hipStream_t s) {
-    return br_version() == 1 ? launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s)
-                             : launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
+    switch (br_version()) {
+    case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
+    case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
+    default: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
+    }
 }
 
 }  // namespace tfhe_amd
@@ -425,8 +429,10 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, s, true);
-    HIPCHK(br_version() == 1 ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
-                             : launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s));
+    const int v = br_version();
+    HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
+           : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
+                    : launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
 
@@ -529,11 +535,13 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version != 1 && br_version != 2) return TFHE_AMD_E_ARG;
+    if (br_version < 1 || br_version > 3) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }
 
 extern "C" const char *tfhe_amd_version(void) {
-    return br_version() == 1 ? "tfhe_amd gfx950 ntt2x30 br-v1 ks-v1" : "tfhe_amd gfx950 ntt2x30 br-v2 ks-v1";
+    static const char *names[] = {"", "tfhe_amd gfx950 ntt2x27 br-v1 ks-v2", "tfhe_amd gfx950 ntt2x27 br-v2 ks-v2",
+                                  "tfhe_amd gfx950 ntt2x27 br-v3 ks-v2"};
+    return names[br_version()];
 }

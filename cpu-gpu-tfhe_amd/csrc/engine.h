@@ -45,7 +45,11 @@ hipError_t launch_blind_rotate_v2(const DeviceKey &key, int B, int halves, const
                                   int32_t *u_a, int32_t *u_b, hipStream_t s);
 hipError_t launch_blind_rotate_v2_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
-// which blind-rotation kernel runs: 2 (default) or 1 (env TFHE_AMD_BR=1)
+hipError_t launch_blind_rotate_v3(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v3_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                        const int32_t *bara, hipStream_t s);
+// which blind-rotation kernel runs: 1, 2 or 3 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).

@@ -20,7 +20,8 @@ except ImportError:  # pragma: no cover - the C ABI itself does not need torch
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtfhe_amd.so")
+# TFHE_AMD_LIB selects an alternative build of the same library (A/B kernel variants)
+LIB_PATH = os.environ.get("TFHE_AMD_LIB") or os.path.join(HERE, "lib", "libtfhe_amd.so")
 
 N, n_lwe, KPL, KS_T, KS_BASE = 1024, 500, 4, 8, 4
 GATES = {"NAND": 0, "OR": 1, "AND": 2, "XOR": 3, "XNOR": 4, "NOR": 5,

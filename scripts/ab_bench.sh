@@ -1,0 +1,9 @@
+#!/usr/bin/env bash
+# A/B of library variants in one GPU session: scripts/ab_bench.sh name1 name2 ... ("base" = lib/)
+set -u
+for n in "$@"; do
+  if [ "$n" = base ]; then lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so; else lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so; fi
+  TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$n.log 2>&1
+  rc=$?; echo "$n rc=$rc"; [ $rc -ge 124 ] && exit $rc
+done
+exit 0
