@@ -65,13 +65,32 @@ def cpu_baseline(bk, ksk, rng, target_s):
             "sample": f"{B} bootsNAND (random LWE inputs) on {threads} OpenMP threads, {t:.1f} s"}
 
 
+def pmc_traffic(engine, batch):
+    """HBM bytes per blind-rotation launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, written by scripts/pmc_summary.py from separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per the gfx950 correction for
+    16-B-per-lane streaming reads).  None when no summary matches this engine/batch."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        s = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    k = s.get("kernels", {}).get("blind_rotate")
+    if not k or s.get("engine") != engine or s.get("batch") != batch:
+        return None
+    return k["hbm_bytes_per_launch"]
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
+    import shard
     import tfhe_amd as T
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and int(os.environ.get("RANK", "0")) == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -107,11 +126,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device="cuda")
 
     # correctness guard on the last step's output (truth table; cheap)
     dec = K.decrypt(r_a.cpu().numpy(), r_b.cpu().numpy())
@@ -128,8 +143,7 @@ def main():
     ks_ms = prof["ks_ms"] / max(1, prof["ks_launches"])
     achieved = B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9
 
-    total = B * world * args.steps
-    value = total / elapsed
+    value = shard.weak_scaling_value(B, world, args.steps, elapsed)
     line = {
         "metric": "gate bootstraps/sec (bootsNAND, N=1024)",
         "value": value,
@@ -141,13 +155,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32 (Torus32, exact 2x30-bit CRT NTT)",
+        "dtype": "int32 (Torus32; exact 2x27-bit CRT NTT)",
         "data": "synthetic: random bits encrypted under keys generated from seed {314,1592,657}",
         "config": {"workload": f"batch of {B} independent boots{args.gate} per GPU (BASELINE configs[1])",
                    "batch_per_gpu": B, "gate": args.gate, "params": "n=500 N=1024 k=1 l=2 Bgbit=10 ks_t=8 ks_basebit=2",
                    "parallelism": f"shard{world} (independent ciphertexts, no collective)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
                      "kernel": "k_blind_rotate", "kernel_ms": br_ms, "keyswitch_ms": ks_ms,
                      "algorithmic_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP},
         "truth_table_ok": truth_ok,
