@@ -355,7 +355,10 @@ __device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, in
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kV2Threads) void k_blind_rotate_v2(V2Args g, int B, BrInput in0, BrInput in1,
+#ifndef TFHE_AMD_V2_MINW
+#define TFHE_AMD_V2_MINW 1     // waves/SIMD floor for the register allocator (A/B builds: 2, 3)
+#endif
+__global__ __launch_bounds__(kV2Threads, TFHE_AMD_V2_MINW) void k_blind_rotate_v2(V2Args g, int B, BrInput in0, BrInput in1,
                                                                 int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
     __shared__ V2Shared sh;
