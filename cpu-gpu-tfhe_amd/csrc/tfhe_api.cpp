@@ -31,8 +31,10 @@
 #include "params.h"
 #include "../../include/tfhe/tfhe.h"
 #include "../../include/tfhe_amd.h"
+#include "api_internal.h"
 
 using namespace tfhe_amd;
+using namespace tfhe_amd::api;
 
 TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary);   // engine.cpp
 
@@ -88,28 +90,37 @@ EXPORT Torus32 modSwitchToTorus32(int mu, int Msize) {
 
 // ------------------------------------------------------------------ params
 // tfhe_gate_bootstrapping.cu:25-55; tgsw.cu:7-29; tlwe.cu (extracted params n = k N)
+// (ParamsImpl is declared in api_internal.h; alphas are arguments because parameter sets
+// read back from a file carry the %.8lf-rounded values, tfhe_generic_streams.cu:37-41)
 
-struct ParamsImpl {
-    LweParams in_out{kn, kKsStdev, kMaxStdev};
-    TLweParams accum{kN, kK, kBkStdev, kMaxStdev, LweParams{kN * kK, kBkStdev, kMaxStdev}};
-    Torus32 h[kL];
-    TGswParams tgsw{kL, kBgbit, 1 << kBgbit, (1 << kBgbit) / 2, (1u << kBgbit) - 1, &accum, kKpl, h, kDecompOffset};
-    TFheGateBootstrappingParameterSet set{kKsT, kKsBasebit, &in_out, &tgsw};
-    ParamsImpl() {
-        for (int i = 0; i < kL; ++i) h[i] = Torus32(1u << (32 - (i + 1) * kBgbit));
-    }
-};
+ParamsImpl::ParamsImpl(double lwe_alpha_min, double lwe_alpha_max, double tlwe_alpha_min, double tlwe_alpha_max)
+    : in_out{kn, lwe_alpha_min, lwe_alpha_max},
+      accum{kN, kK, tlwe_alpha_min, tlwe_alpha_max, LweParams{kN * kK, tlwe_alpha_min, tlwe_alpha_max}},
+      tgsw{kL, kBgbit, 1 << kBgbit, (1 << kBgbit) / 2, (1u << kBgbit) - 1, &accum, kKpl, h, kDecompOffset},
+      set{kKsT, kKsBasebit, &in_out, &tgsw} {
+    for (int i = 0; i < kL; ++i) h[i] = Torus32(1u << (32 - (i + 1) * kBgbit));
+}
 
 static std::mutex g_params_mu;
 static std::map<const TFheGateBootstrappingParameterSet *, ParamsImpl *> g_params;
 
-EXPORT TFheGateBootstrappingParameterSet *new_default_gate_bootstrapping_parameters(int minimum_lambda) {
-    if (minimum_lambda > 128)
-        die_dramatically("Sorry, for now, the parameters are only implemented for about 128bit of security!");
-    ParamsImpl *p = new ParamsImpl();
+TFheGateBootstrappingParameterSet *tfhe_amd::api::register_params(ParamsImpl *p) {
     std::lock_guard<std::mutex> lk(g_params_mu);
     g_params[&p->set] = p;
     return &p->set;
+}
+
+const ParamsImpl *tfhe_amd::api::params_of(const TFheGateBootstrappingParameterSet *params) {
+    std::lock_guard<std::mutex> lk(g_params_mu);
+    auto it = g_params.find(params);
+    if (it == g_params.end()) die_dramatically("tfhe_amd: unknown parameter set");
+    return it->second;
+}
+
+EXPORT TFheGateBootstrappingParameterSet *new_default_gate_bootstrapping_parameters(int minimum_lambda) {
+    if (minimum_lambda > 128)
+        die_dramatically("Sorry, for now, the parameters are only implemented for about 128bit of security!");
+    return register_params(new ParamsImpl());
 }
 
 EXPORT void delete_gate_bootstrapping_parameters(TFheGateBootstrappingParameterSet *params) {
@@ -152,13 +163,13 @@ EXPORT void delete_gate_bootstrapping_ciphertext_array(int nbelems, LweSample *s
     delete_LweSample_array(nbelems, samples);
 }
 
-static LweKey *new_LweKey(const LweParams *params) {
+LweKey *tfhe_amd::api::new_LweKey(const LweParams *params) {
     LweKey *k = (LweKey *)malloc(sizeof(LweKey));
     *const_cast<const LweParams **>(&k->params) = params;
     k->key = (int *)calloc((size_t)params->n, sizeof(int));
     return k;
 }
-static void delete_LweKey(LweKey *k) {
+void tfhe_amd::api::delete_LweKey(LweKey *k) {
     if (!k) return;
     free(k->key);
     free(k);
@@ -320,7 +331,7 @@ static void ksk_flatten(const LweKeySwitchKey *ks, int32_t *out) {
             }
 }
 
-static LweBootstrappingKey *new_bk(const ParamsImpl *P) {
+LweBootstrappingKey *tfhe_amd::api::new_bk(const ParamsImpl *P) {
     BkImpl *k = new BkImpl{LweBootstrappingKey{&P->in_out, &P->tgsw, &P->accum, &P->accum.extracted_lweparams,
                                                nullptr, nullptr},
                            {}, {}, {}, {}, {}, nullptr};
@@ -359,7 +370,7 @@ static void bk_flatten(const LweBootstrappingKey *bk, int32_t *out) {
 
 // new_LweBootstrappingKeyFFT (lwe-bootstrapping-functions-fft.cu:2201 -> :60-89): copy the KSK,
 // keep the coefficient BK for the device-side NTT conversion.
-static LweBootstrappingKeyFFT *new_bkfft(const LweBootstrappingKey *bk) {
+LweBootstrappingKeyFFT *tfhe_amd::api::new_bkfft(const LweBootstrappingKey *bk) {
     BkFFTImpl *f = new BkFFTImpl{LweBootstrappingKeyFFT{bk->in_out_params, bk->bk_params, bk->accum_params,
                                                         bk->extract_params, nullptr, nullptr},
                                  {}, nullptr};
@@ -389,11 +400,14 @@ static void delete_bkfft(LweBootstrappingKeyFFT *k) {
     delete f;
 }
 
-struct TGswKeyImpl {
-    TGswKey pub;
-    std::vector<int> coefs;
-    IntPolynomial poly;
-};
+TGswKey *tfhe_amd::api::new_tgsw_key(const ParamsImpl *P) {
+    TGswKeyImpl *gk = new TGswKeyImpl{TGswKey{&P->tgsw, &P->accum, nullptr, TLweKey{&P->accum, nullptr}},
+                                      std::vector<int>((size_t)kN * kK), IntPolynomial{kN, nullptr}};
+    gk->poly.coefs = gk->coefs.data();
+    gk->pub.key = &gk->poly;
+    gk->pub.tlwe_key.key = &gk->poly;
+    return &gk->pub;
+}
 
 // lweCreateKeySwitchKey (lwe-keyswitch-functions.cu:890-942)
 static void create_ksk_nolock(LweKeySwitchKey *result, const int *in_key /*kN*/, const LweKey *out_key) {
@@ -439,21 +453,11 @@ static void tlwe_encrypt_zero_nolock(TLweSample *r, double alpha, const int *key
 
 EXPORT TFheGateBootstrappingSecretKeySet *
 new_random_gate_bootstrapping_secret_keyset(const TFheGateBootstrappingParameterSet *params) {
-    const ParamsImpl *P;
-    {
-        std::lock_guard<std::mutex> lk(g_params_mu);
-        auto it = g_params.find(params);
-        if (it == g_params.end()) die_dramatically("tfhe_amd: unknown parameter set");
-        P = it->second;
-    }
+    const ParamsImpl *P = params_of(params);
     std::lock_guard<std::mutex> lk(g_rng_mu);
     LweKey *lwe_key = new_LweKey(params->in_out_params);
     lweKeyGen_nolock(lwe_key);                                              // :60
-    TGswKeyImpl *gk = new TGswKeyImpl{TGswKey{&P->tgsw, &P->accum, nullptr, TLweKey{&P->accum, nullptr}},
-                                      std::vector<int>(kN), IntPolynomial{kN, nullptr}};
-    gk->poly.coefs = gk->coefs.data();
-    gk->pub.key = &gk->poly;
-    gk->pub.tlwe_key.key = &gk->poly;
+    TGswKeyImpl *gk = reinterpret_cast<TGswKeyImpl *>(new_tgsw_key(P));
     {   // tGswKeyGen -> tLweKeyGen (tlwe-functions.cu:15-23)
         std::uniform_int_distribution<int> distribution(0, 1);
         for (int j = 0; j < kN; ++j) gk->coefs[j] = distribution(generator);

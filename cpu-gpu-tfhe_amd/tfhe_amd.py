@@ -76,6 +76,20 @@ def _load():
     L.modSwitchToTorus32.restype = ctypes.c_int32
     L.modSwitchFromTorus32.restype = ctypes.c_int
     L.lwePhase.restype = ctypes.c_int32
+    # tfhe_io.h (FILE* entry points)
+    for f in ("export_tfheGateBootstrappingSecretKeySet_toFile", "export_tfheGateBootstrappingCloudKeySet_toFile",
+              "export_tfheGateBootstrappingParameterSet_toFile"):
+        getattr(L, f).argtypes = [_VP, _VP]
+    for f in ("new_tfheGateBootstrappingSecretKeySet_fromFile", "new_tfheGateBootstrappingCloudKeySet_fromFile",
+              "new_tfheGateBootstrappingParameterSet_fromFile"):
+        getattr(L, f).argtypes = [_VP]
+        getattr(L, f).restype = _VP
+    L.export_gate_bootstrapping_ciphertext_toFile.argtypes = [_VP, _VP, _VP]
+    L.import_gate_bootstrapping_ciphertext_fromFile.argtypes = [_VP, _VP, _VP]
+    L.new_gate_bootstrapping_ciphertext_array.argtypes = [ctypes.c_int, _VP]
+    L.new_gate_bootstrapping_ciphertext_array.restype = _VP
+    L.delete_gate_bootstrapping_ciphertext_array.argtypes = [ctypes.c_int, _VP]
+    L.delete_gate_bootstrapping_cloud_keyset.argtypes = [_VP]
     return L
 
 
@@ -102,19 +116,85 @@ def i32(x):
     return np.ascontiguousarray(np.asarray(x, dtype=np.int64).astype(np.int32))
 
 
+# --------------------------------------------------------------------- files (tfhe_io.h)
+
+_libc = ctypes.CDLL(None)
+_libc.fopen.restype = _VP
+_libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+_libc.fclose.argtypes = [_VP]
+
+
+class _File:
+    """FILE* for the tfhe_io.h entry points (they take C stdio streams, like the reference)."""
+
+    def __init__(self, path, mode):
+        self.f = _libc.fopen(os.fsencode(path), mode.encode())
+        if not self.f:
+            raise OSError(f"cannot open {path} ({mode})")
+
+    def __enter__(self):
+        return self.f
+
+    def __exit__(self, *exc):
+        _libc.fclose(self.f)
+
+
+class LweSampleC(ctypes.Structure):
+    """struct LweSample (lwesamples.h:18-29)."""
+    _fields_ = [("a", _I32P), ("b", ctypes.c_int32), ("current_variance", ctypes.c_double)]
+
+
+def write_ciphertexts(path, params, a, b, variance=0.0, mode="wb"):
+    """export_gate_bootstrapping_ciphertext_toFile for each row of the SoA batch (a [B][n], b [B])."""
+    a = i32(a); b = i32(b); B = a.shape[0]
+    arr = lib.new_gate_bootstrapping_ciphertext_array(B, params)
+    try:
+        s = (LweSampleC * B).from_address(arr)
+        with _File(path, mode) as f:
+            for i in range(B):
+                ctypes.memmove(s[i].a, a[i].ctypes.data, 4 * n_lwe)
+                s[i].b = int(b[i]); s[i].current_variance = float(variance)
+                lib.export_gate_bootstrapping_ciphertext_toFile(f, ctypes.byref(s[i]), params)
+    finally:
+        lib.delete_gate_bootstrapping_ciphertext_array(B, arr)
+
+
+def read_ciphertexts(path, params, B):
+    """import_gate_bootstrapping_ciphertext_fromFile B times -> (a [B][n], b [B], variance [B])."""
+    arr = lib.new_gate_bootstrapping_ciphertext_array(B, params)
+    a = np.zeros((B, n_lwe), np.int32); b = np.zeros(B, np.int32); v = np.zeros(B)
+    try:
+        s = (LweSampleC * B).from_address(arr)
+        with _File(path, "rb") as f:
+            for i in range(B):
+                lib.import_gate_bootstrapping_ciphertext_fromFile(f, ctypes.byref(s[i]), params)
+                ctypes.memmove(a[i].ctypes.data, s[i].a, 4 * n_lwe)
+                b[i] = s[i].b; v[i] = s[i].current_variance
+    finally:
+        lib.delete_gate_bootstrapping_ciphertext_array(B, arr)
+    return a, b, v
+
+
 # --------------------------------------------------------------------- keys (host)
 
 class SecretKeyset:
     """new_random_gate_bootstrapping_secret_keyset (tfhe_gate_bootstrapping.cu:57-68) seeded
     through tfhe_random_generator_setSeed; exposes the key material as numpy arrays."""
 
-    def __init__(self, seed=(314, 1592, 657)):
-        s = (ctypes.c_uint32 * len(seed))(*seed)
-        lib.tfhe_random_generator_setSeed(s, len(seed))
-        self.params = lib.new_default_gate_bootstrapping_parameters(110)
-        self.h = lib.new_random_gate_bootstrapping_secret_keyset(self.params)
+    def __init__(self, seed=(314, 1592, 657), path=None):
+        """seeded keygen, or (path=...) new_tfheGateBootstrappingSecretKeySet_fromFile."""
+        if path is None:
+            s = (ctypes.c_uint32 * len(seed))(*seed)
+            lib.tfhe_random_generator_setSeed(s, len(seed))
+            self.own_params = lib.new_default_gate_bootstrapping_parameters(110)
+            self.h = lib.new_random_gate_bootstrapping_secret_keyset(self.own_params)
+        else:
+            self.own_params = None            # belongs to the keyset read from the file
+            with _File(path, "rb") as f:
+                self.h = lib.new_tfheGateBootstrappingSecretKeySet_fromFile(f)
         if not self.h:
             raise TfheAmdError("keygen failed")
+        self.params = ctypes.c_void_p.from_address(self.h).value     # key->params
         self.bk = np.zeros((n_lwe, KPL, 2, N), np.int32)
         self.ksk = np.zeros((N, KS_T, KS_BASE, n_lwe + 1), np.int32)
         self.lwe_key = np.zeros(n_lwe, np.int32)
@@ -123,6 +203,16 @@ class SecretKeyset:
         _check(lib.tfhe_amd_export_lwe_key(ctypes.c_void_p(self.h), _p(self.lwe_key)), "export_lwe_key")
         self.tlwe_key = np.zeros(N, np.int32)
         _check(lib.tfhe_amd_export_tlwe_key(ctypes.c_void_p(self.h), _p(self.tlwe_key)), "export_tlwe_key")
+
+    def save(self, path):
+        """export_tfheGateBootstrappingSecretKeySet_toFile"""
+        with _File(path, "wb") as f:
+            lib.export_tfheGateBootstrappingSecretKeySet_toFile(f, self.h)
+
+    def save_cloud(self, path):
+        """export_tfheGateBootstrappingCloudKeySet_toFile(F, &key->cloud)"""
+        with _File(path, "wb") as f:
+            lib.export_tfheGateBootstrappingCloudKeySet_toFile(f, self._cloud())
 
     def _cloud(self):
         # &key->cloud: TFheGateBootstrappingSecretKeySet = {params*, lwe_key*, tgsw_key*, cloud}
@@ -136,6 +226,9 @@ class SecretKeyset:
         if self.h:
             lib.delete_gate_bootstrapping_secret_keyset(self.h)
             self.h = None
+        if self.own_params:
+            lib.delete_gate_bootstrapping_parameters(self.own_params)
+            self.own_params = None
 
     # numpy-side encryption with the same secret (fast path for big batches; the product's
     # bootsSymEncrypt is covered by its own test)
@@ -161,6 +254,36 @@ class SecretKeyset:
         u_a = np.asarray(u_a).astype(np.int64)
         ph = (np.asarray(u_b).astype(np.int64) - u_a @ self.tlwe_key.astype(np.int64)) & 0xFFFFFFFF
         return ph.astype(np.uint32).view(np.int32)
+
+
+class CloudKeyset:
+    """new_tfheGateBootstrappingCloudKeySet_fromFile (tfhe_io.cu:1117): what cloud.cpp loads."""
+
+    def __init__(self, path):
+        with _File(path, "rb") as f:
+            self.h = lib.new_tfheGateBootstrappingCloudKeySet_fromFile(f)
+        if not self.h:
+            raise TfheAmdError(f"cannot read cloud key {path}")
+        self.params = ctypes.c_void_p.from_address(self.h).value      # bk->params
+
+    def save(self, path):
+        with _File(path, "wb") as f:
+            lib.export_tfheGateBootstrappingCloudKeySet_toFile(f, self.h)
+
+    def export_bk(self):
+        bk = np.zeros((n_lwe, KPL, 2, N), np.int32)
+        _check(lib.tfhe_amd_export_bk(ctypes.c_void_p(self.h), _p(bk)), "export_bk")
+        return bk
+
+    def export_ksk(self):
+        ksk = np.zeros((N, KS_T, KS_BASE, n_lwe + 1), np.int32)
+        _check(lib.tfhe_amd_export_ksk(ctypes.c_void_p(self.h), _p(ksk)), "export_ksk")
+        return ksk
+
+    def close(self):
+        if self.h:
+            lib.delete_gate_bootstrapping_cloud_keyset(self.h)
+            self.h = None
 
 
 # --------------------------------------------------------------------- device context

@@ -24,6 +24,11 @@
 #define TFHE_AMD_TFHE_H
 
 #include "tfhe_core.h"
+#include "tfhe_io.h"      /* the reference tfhe.h includes it too (gpuParallel/tfhe.h:26) */
+#ifdef __cplusplus
+#include <cmath>          /* callers rely on it arriving via tfhe.h -> numeric_functions.h:10
+                             (<random>); cloud.cpp:43 calls pow() without including it */
+#endif
 
 struct LweParams {
     const int n;

@@ -16,7 +16,7 @@ import tfhe_amd as T
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 HEADERS = [os.path.join(REPO, "include", "tfhe", "tfhe.h"), os.path.join(REPO, "include", "tfhe", "tfhe_core.h"),
-           os.path.join(REPO, "include", "tfhe_amd.h")]
+           os.path.join(REPO, "include", "tfhe", "tfhe_io.h"), os.path.join(REPO, "include", "tfhe_amd.h")]
 G = np.load(os.path.join(HERE, "golden", "ref_leaf_vectors.npz"))
 
 
