@@ -21,6 +21,7 @@
 //  * the two primes meet in a CRT exchange through LDS; the accumulator lives in LDS.
 #include "engine.h"
 #include "modarith.h"
+#include "ntt_wave.h"
 
 #include <cstdlib>
 
@@ -29,220 +30,6 @@ namespace tfhe_amd {
 namespace {
 
 constexpr int kV2Threads = 128;
-constexpr int kPadRow = kN + 64;   // padded scratch row: index j at word j + 4 (j >> 6)
-
-__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
-
-// 16-B LDS vector that may alias the uint32_t view of the same scratch (the transposes write
-// b32 and read b128 and vice versa: without may_alias, TBAA lets the compiler hoist the b128
-// reads above the b32 writes of the same wave)
-typedef uint32_t lds_u32x4 __attribute__((ext_vector_type(4), may_alias));
-
-// Shoup product y * w mod q, lazy: [0, 2q) for any y < 2^32.  y*w - qh*q (mod 2^32) is
-// folded into one v_mad_u64_u32: qh * (2^32 - q) + lo(y*w).
-__device__ __forceinline__ uint32_t shoup_lazy(uint32_t y, uint32_t w, uint32_t wp, uint32_t negq) {
-    const uint32_t qh = __umulhi(y, wp);
-    return (uint32_t)((uint64_t)qh * negq + (uint32_t)(y * w));
-}
-// Cooley-Tukey (forward) butterfly WITHOUT reductions: inputs < B -> outputs < B + 2q.
-// Digits enter < 2q, so after the 10 stages every value is < 22q < 2^32 (q < 2^27).
-__device__ __forceinline__ void bf_ct(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t negq,
-                                      uint32_t q2) {
-    const uint32_t t = shoup_lazy(y, w, wp, negq);    // [0, 2q)
-    const uint32_t u = x;
-    x = u + t;
-    y = u - t + q2;
-}
-// Gentleman-Sande (inverse) butterfly, Harvey: x, y in [0, 2q) -> [0, 2q)
-__device__ __forceinline__ void bf_gs(uint32_t &x, uint32_t &y, uint32_t w, uint32_t wp, uint32_t negq,
-                                      uint32_t q2) {
-    const uint32_t s = x + y;
-    const uint32_t t = x - y + q2;
-    x = umin32(s, s - q2);
-    y = shoup_lazy(t, w, wp, negq);
-}
-
-// Lanes of one wave exchange values through LDS in the transposes.  Single-thread
-// semantics let the compiler hoist a lane's read above another lane's write whenever it
-// can prove the two addresses differ FOR THE SAME LANE (it did, e.g. load_B(r < 8) above
-// the last store_A: every coefficient came out wrong).  A wavefront-scope release/acquire
-// pair around a wave barrier pins the order; LDS itself executes one wave's DS
-// instructions in order.
-__device__ __forceinline__ void wave_lds_sync() {
-#ifdef TFHE_AMD_LDS_COMPILER_BARRIER
-    asm volatile("" ::: "memory");      // experiment: rely on in-order LDS, compiler fence only
-#else
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
-}
-
-// ---- layout transposes through the per-wave scratch (one polynomial)
-__device__ __forceinline__ void store_A(uint32_t *sc, const uint32_t (&x)[16], int L) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[L + 68 * r] = x[r];            // j = L + 64 r
-}
-__device__ __forceinline__ void load_A(const uint32_t *sc, uint32_t (&x)[16], int L) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) x[r] = sc[L + 68 * r];
-}
-__device__ __forceinline__ int base_B(int L) { return (L & 3) + 68 * (L >> 2); }
-__device__ __forceinline__ void store_B(uint32_t *sc, const uint32_t (&x)[16], int L) {
-    uint32_t *p = sc + base_B(L);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p[4 * r] = x[r];                   // j = (L&3) | r<<2 | (L>>2)<<6
-}
-__device__ __forceinline__ void load_B(const uint32_t *sc, uint32_t (&x)[16], int L) {
-    const uint32_t *p = sc + base_B(L);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) x[r] = p[4 * r];
-}
-__device__ __forceinline__ int base_C(int L) { return 16 * L + 4 * (L >> 2); }
-__device__ __forceinline__ void store_C(uint32_t *sc, const uint32_t (&x)[16], int L) {
-    lds_u32x4 *p = reinterpret_cast<lds_u32x4 *>(sc + base_C(L));    // j = 16 L + r
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        lds_u32x4 t;
-        t.x = x[4 * v]; t.y = x[4 * v + 1]; t.z = x[4 * v + 2]; t.w = x[4 * v + 3];
-        p[v] = t;
-    }
-}
-__device__ __forceinline__ void load_C(const uint32_t *sc, uint32_t (&x)[16], int L) {
-    const lds_u32x4 *p = reinterpret_cast<const lds_u32x4 *>(sc + base_C(L));
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const lds_u32x4 t = p[v];
-        x[4 * v] = t.x; x[4 * v + 1] = t.y; x[4 * v + 2] = t.z; x[4 * v + 3] = t.w;
-    }
-}
-
-// ---- forward NTT of NP polys (layout A in, layout C out), values < 2q in, < 22q out
-template <int NP>
-__device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
-                                        const uint2 *__restrict__ ts, int L, uint32_t q) {
-    const uint32_t q2 = 2 * q, negq = 0u - q;
-#pragma unroll
-    for (int K = 9; K >= 6; --K) {                     // layout A, uniform twiddles
-        const int d = 1 << (K - 6);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        store_A(sc, x[p], L);
-        wave_lds_sync();
-        load_B(sc, x[p], L);
-        wave_lds_sync();
-    }
-    int slot = 0;
-#pragma unroll
-    for (int K = 5; K >= 2; --K) {                     // layout B, per-lane twiddles
-        const int d = 1 << (K - 2), cnt = 1 << (5 - K);
-        uint2 tw[8];
-#pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
-        slot += cnt;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tw[r >> (K - 1)];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        store_B(sc, x[p], L);
-        wave_lds_sync();
-        load_C(sc, x[p], L);
-        wave_lds_sync();
-    }
-#pragma unroll
-    for (int K = 1; K >= 0; --K) {                     // layout C
-        const int d = 1 << K, cnt = 1 << (3 - K);
-        uint2 tw[8];
-#pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
-        slot += cnt;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tw[r >> (K + 1)];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_ct(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-}
-
-// ---- inverse NTT of NP polys (layout C in, layout A out), values [0,2q) -> [0,2q)
-template <int NP>
-__device__ __forceinline__ void ntt_inv(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
-                                        const uint2 *__restrict__ ts, int L, uint32_t q) {
-    const uint32_t q2 = 2 * q, negq = 0u - q;
-    int slot = 0;
-#pragma unroll
-    for (int K = 0; K <= 3; ++K) {                     // layout C
-        const int d = 1 << K, cnt = 1 << (3 - K);
-        uint2 tw[8];
-#pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
-        slot += cnt;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tw[r >> (K + 1)];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        store_C(sc, x[p], L);
-        wave_lds_sync();
-        load_B(sc, x[p], L);
-        wave_lds_sync();
-    }
-#pragma unroll
-    for (int K = 4; K <= 5; ++K) {                     // layout B
-        const int d = 1 << (K - 2), cnt = 1 << (5 - K);
-        uint2 tw[2];
-#pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[(slot + g) * 64];
-        slot += cnt;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tw[r >> (K - 1)];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        store_B(sc, x[p], L);
-        wave_lds_sync();
-        load_A(sc, x[p], L);
-        wave_lds_sync();
-    }
-#pragma unroll
-    for (int K = 6; K <= 9; ++K) {                     // layout A, uniform twiddles
-        const int d = 1 << (K - 6);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & d) continue;
-            const uint2 t = tu[(1 << (9 - K)) + (r >> (K - 5))];
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bf_gs(x[p][r], x[p][r + d], t.x, t.y, negq, q2);
-        }
-    }
-}
-
 struct V2Shared {
     uint32_t acc[2][kN];               // TLWE accumulator (a, b)
     uint32_t scratch[2][kPadRow];      // one per wave (prime)
@@ -308,7 +95,11 @@ __device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, in
         }
     ntt_fwd<4>(D, sc, g.tu_f + 16 * s, g.ts_f + s * 27 * 64 + L, L, q);
     // pointwise MAC with BK_i (layout C: reg r = 4 v + e <-> j = 16 L + r)
+#ifdef TFHE_AMD_DIAG_BK
+    const uint4 *bk4 = reinterpret_cast<const uint4 *>(g.bk + ((size_t)(0 * 2 + s) * 8) * kN) + L;
+#else
     const uint4 *bk4 = reinterpret_cast<const uint4 *>(g.bk + ((size_t)(i * 2 + s) * 8) * kN) + L;
+#endif
     const uint32_t qinv = s ? g.qinv_neg1 : g.qinv_neg0;
     uint32_t O[2][16];
 #pragma unroll
@@ -602,7 +393,7 @@ __global__ __launch_bounds__(256) void k_bk_v1_to_v2(const uint32_t *__restrict_
 void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f, uint2 *ts_i) {
     for (int s = 0; s < 2; ++s) {
         for (int idx = 0; idx < 16; ++idx) {
-            tu_f[s * 16 + idx] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+            tu_f[s * 16 + idx] = make_uint2(0u - t.psi[s][idx], t.psip[s][idx]);   // negated: bf_ct
             tu_i[s * 16 + idx] = make_uint2(t.ipsi[s][idx], t.ipsip[s][idx]);
         }
         int slot = 0;
@@ -610,13 +401,13 @@ void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f
             for (int g = 0; g < (1 << (5 - K)); ++g, ++slot)
                 for (int L = 0; L < 64; ++L) {
                     const int idx = (1 << (9 - K)) + ((L >> 2) << (5 - K)) + g;
-                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(0u - t.psi[s][idx], t.psip[s][idx]);
                 }
         for (int K = 1; K >= 0; --K)
             for (int g = 0; g < (1 << (3 - K)); ++g, ++slot)
                 for (int L = 0; L < 64; ++L) {
                     const int idx = (1 << (9 - K)) + (L << (3 - K)) + g;
-                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(t.psi[s][idx], t.psip[s][idx]);
+                    ts_f[(s * 27 + slot) * 64 + L] = make_uint2(0u - t.psi[s][idx], t.psip[s][idx]);
                 }
         slot = 0;
         for (int K = 0; K <= 3; ++K)

@@ -1,0 +1,275 @@
+// blind_rotate_v4.hip — v4 blind rotation: v2's register-resident layout with fewer VALU
+// instructions per CMux step (the v2 kernel is VALU-issue bound: its time tracks its
+// instruction count).
+//
+// Same contract as v2 (tfhe_blindRotate_FFT + extraction, lwe-bootstrapping-functions-fft.cu
+// :676-737, 1408-1456, 1834-1870; tGswFFTExternMulToTLwe tgsw-fft-operations.cu:124-264).
+// Changes against v2, all exact (scripts/emu_v4.py checks the index math and the bounds):
+//  * inverse transform = Cooley-Tukey DIT on the bit-reversed slots + a psi^-n post-twist
+//    (5 VALU per butterfly, no reductions: < 23.75q) instead of Harvey Gentleman-Sande (8);
+//  * the MAC's REDC result stays lazy (< 3.75q), the inverse output stays lazy ([0, 2q)) and
+//    the CRT lift takes both residues lazily;
+//  * the accumulator is kept as a periodic negacyclic extension E[k] = +-acc[k mod N]
+//    (k < 3N, sign - when k mod 2N >= N): X^a * ACC at coefficient j is E[(j - a) mod 2N + ...]
+//    read with immediate offsets, so the rotation costs no address or sign arithmetic.
+#include "engine.h"
+#include "modarith.h"
+#include "ntt_wave.h"
+
+namespace tfhe_amd {
+
+namespace {
+
+constexpr int kV4Threads = 128;
+constexpr int kExt = 3 * kN;
+
+struct V4Shared {
+    uint32_t E[2][kExt];               // periodic negacyclic accumulator (a, b), 24 KB
+    uint32_t scratch[2][kPadRow];      // one per wave (prime)
+    int bara[512];
+    int barb;
+};
+
+struct V4Args {
+    const uint32_t *bk;   // [kn][2][2 c][4 p][4 v][64 L][4 e]   (v2 layout)
+    const uint2 *tu_f;    // [2][16] uniform forward twiddles (negated)
+    const uint2 *ts_f;    // [2][27][64] forward streams (negated)
+    const uint2 *tu_i;    // [2][16] inverse-CT uniform twiddles (negated)
+    const uint2 *ts_i;    // [2][27][64] inverse-CT streams (negated)
+    const uint2 *tpost;   // [2][16][64] psi^-(L + 64 r), positive
+    uint32_t qinv_neg0, qinv_neg1, crt_h, crt_hp;
+};
+
+__device__ __forceinline__ void e_store(uint32_t *E, int j, uint32_t v) {
+    E[j] = v;
+    E[j + kN] = 0u - v;
+    E[j + 2 * kN] = v;
+}
+
+// centred CRT lift of lazy residues x0 in [0, 2 q0), x1 in [0, 2 q1), reduced mod 2^32.
+// The exact external-product coefficient c has |c| < 2^52 << q0 q1 / 2, so the lift
+// x0 + q0 tc with tc = (x1 - x0) q0^-1 mod q1 taken in (-q1/2, q1/2] equals c.
+__device__ __forceinline__ uint32_t crt_lazy(uint32_t x0, uint32_t x1, uint32_t h, uint32_t hp) {
+    const uint32_t d = x1 + 3u * kQ1 - x0;                      // (q1, 5 q1)
+    const uint32_t t0 = shoup_lazy(d, h, hp, 0u - kQ1);         // [0, 2 q1)
+    const uint32_t t = umin32(t0, t0 - kQ1);                    // [0, q1)
+    const uint32_t tc = t > (kQ1 - 1) / 2 ? t - kQ1 : t;
+    return x0 + kQ0 * tc;
+}
+
+template <int S>
+__device__ __forceinline__ void crt4_give(V4Shared &sh, const uint32_t (&O)[2][16], int L) {
+    uint32_t *mine = sh.scratch[S];
+    constexpr int give = 8 * (1 - S);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) mine[(c * 8 + rr) * 64 + L] = O[c][give + rr];
+}
+template <int S>
+__device__ __forceinline__ void crt4_take(V4Shared &sh, const uint32_t (&O)[2][16], int L, const V4Args &g) {
+    const uint32_t *other = sh.scratch[1 - S];
+    constexpr int keep = 8 * S;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+            const uint32_t xo = other[(c * 8 + rr) * 64 + L];
+            const uint32_t xm = O[c][keep + rr];
+            const uint32_t x0 = S == 0 ? xm : xo, x1 = S == 0 ? xo : xm;
+            const int j = L + 64 * (keep + rr);
+            e_store(sh.E[c], j, sh.E[c][j] + crt_lazy(x0, x1, g.crt_h, g.crt_hp));
+        }
+}
+
+// one CMux step for key index i and rotation a (1..2N-1); called by both waves
+__device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, int a, int s, int L) {
+    const uint32_t q = s ? kQ1 : kQ0;
+    uint32_t *sc = sh.scratch[s];
+    // (X^a - 1) ACC + gadget decomposition (tgsw-functions.cu:300-413), layout A; digits
+    // lifted to [q - 512, q + 511]
+    uint32_t D[4][16];
+    const int base = (L - a) & (k2N - 1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t t = sh.E[c][base + 64 * r] - sh.E[c][L + 64 * r] + kDecompOffset;
+            D[2 * c][r] = ((t >> 22) & 1023u) + (q - 512u);
+            D[2 * c + 1][r] = ((t >> 12) & 1023u) + (q - 512u);
+        }
+    ntt_fwd<4>(D, sc, g.tu_f + 16 * s, g.ts_f + s * 27 * 64 + L, L, q);
+    // pointwise MAC with BK_i (layout C: reg r = 4 v + e <-> slot 16 L + r), REDC lazy
+    const uint4 *bk4 = reinterpret_cast<const uint4 *>(g.bk + ((size_t)(i * 2 + s) * 8) * kN) + L;
+    const uint32_t qinv = s ? g.qinv_neg1 : g.qinv_neg0;
+    uint32_t O[2][16];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uint4 b[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) b[p] = bk4[(c * 4 + p) * 256 + v * 64];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t b0 = e == 0 ? b[0].x : e == 1 ? b[0].y : e == 2 ? b[0].z : b[0].w;
+                const uint32_t b1 = e == 0 ? b[1].x : e == 1 ? b[1].y : e == 2 ? b[1].z : b[1].w;
+                const uint32_t b2 = e == 0 ? b[2].x : e == 1 ? b[2].y : e == 2 ? b[2].z : b[2].w;
+                const uint32_t b3 = e == 0 ? b[3].x : e == 1 ? b[3].y : e == 2 ? b[3].z : b[3].w;
+                const int r = 4 * v + e;
+                const uint64_t x = (uint64_t)D[0][r] * b0 + (uint64_t)D[1][r] * b1 + (uint64_t)D[2][r] * b2 +
+                                   (uint64_t)D[3][r] * b3;                          // < 88 q^2 < 2^61
+                const uint32_t m = (uint32_t)x * qinv;
+                O[c][r] = (uint32_t)((x + (uint64_t)m * q) >> 32);               // < 3.75 q
+            }
+        }
+    }
+    ntt_inv_ct<2>(O, sc, g.tu_i + 16 * s, g.ts_i + s * 27 * 64 + L, L, q);   // < 23.75 q, layout A
+    {   // post-twist psi^-n (n = L + 64 r) -> [0, 2q)
+        const uint2 *tp = g.tpost + s * 16 * 64 + L;
+        const uint32_t negq = 0u - q;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint2 w = tp[r * 64];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) O[c][r] = shoup_lazy(O[c][r], w.x, w.y, negq);
+        }
+    }
+    if (s == 0) crt4_give<0>(sh, O, L);
+    else crt4_give<1>(sh, O, L);
+    __syncthreads();
+    if (s == 0) crt4_take<0>(sh, O, L, g);
+    else crt4_take<1>(sh, O, L, g);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int B, BrInput in0, BrInput in1,
+                                                                int32_t mu, int32_t *__restrict__ u_a,
+                                                                int32_t *__restrict__ u_b) {
+    __shared__ V4Shared sh;
+    const int tid = threadIdx.x;
+    const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    const int gct = blockIdx.x;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+
+    // gate prologue + modulus switching (boot-gates.cu:98-397; lwe-bootstrapping-functions-fft.cu:1851-1858)
+    for (int i = tid; i < kn; i += kV4Threads) {
+        uint32_t x = (uint32_t)in.sa * (uint32_t)in.x_a[(size_t)idx * kn + i];
+        if (in.sb) x += (uint32_t)in.sb * (uint32_t)in.y_a[(size_t)idx * kn + i];
+        sh.bara[i] = modswitch_2N(x);
+    }
+    if (tid == 0) {
+        uint32_t xb = (uint32_t)in.c + (uint32_t)in.sa * (uint32_t)in.x_b[idx];
+        if (in.sb) xb += (uint32_t)in.sb * (uint32_t)in.y_b[idx];
+        sh.barb = modswitch_2N(xb);
+    }
+    __syncthreads();
+    {   // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431), as its periodic extension
+        const int e = (k2N - sh.barb) & (k2N - 1);
+        for (int k = tid; k < kExt; k += kV4Threads) {
+            sh.E[0][k] = 0;
+            sh.E[1][k] = ((k - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu;
+        }
+    }
+    __syncthreads();
+    for (int i = 0; i < kn; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
+        cmux_v4(sh, g, i, a, s, L);
+    }
+    // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
+    int32_t *ua = u_a + (size_t)gct * kN;
+    for (int j = tid; j < kN; j += kV4Threads) ua[j] = (int32_t)sh.E[0][(k2N - j) & (k2N - 1)];
+    if (tid == 0) u_b[gct] = (int32_t)sh.E[1][0];
+}
+
+__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_debug(V4Args g, int iters, int32_t *__restrict__ acc,
+                                                                      const int32_t *__restrict__ bara) {
+    __shared__ V4Shared sh;
+    const int tid = threadIdx.x;
+    const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
+    for (int j = tid; j < 2 * kN; j += kV4Threads) e_store(sh.E[j >> kLogN], j & (kN - 1), (uint32_t)accg[j]);
+    for (int i = tid; i < iters; i += kV4Threads) sh.bara[i] = bara[(size_t)blockIdx.x * iters + i] & (k2N - 1);
+    __syncthreads();
+    for (int i = 0; i < iters; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;
+        cmux_v4(sh, g, i, a, s, L);
+    }
+    for (int j = tid; j < 2 * kN; j += kV4Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];
+}
+
+unsigned brv10(unsigned x) {
+    unsigned r = 0;
+    for (int i = 0; i < kLogN; i++) { r = (r << 1) | (x & 1); x >>= 1; }
+    return r;
+}
+
+}  // namespace
+
+// Inverse-CT and post-twist tables of the v4 kernel, host side, consumption order.
+// psi^-m for m < N is ipsi[brv(m)] (ntt_tables.h).
+void build_v4_twiddles(const NttTables &t, uint2 *tu_i, uint2 *ts_i, uint2 *tpost) {
+    for (int s = 0; s < 2; ++s) {
+        const uint32_t q = kQ[s];
+        auto ipow = [&](unsigned m) { return t.ipsi[s][brv10(m)]; };
+        auto shp = [&](uint32_t w) { return (uint32_t)(((uint64_t)w << 32) / q); };
+        auto neg = [&](uint32_t w) { return make_uint2(0u - w, shp(w)); };
+        tu_i[s * 16 + 15] = make_uint2(0, 0);
+        for (int S = 0; S <= 3; ++S)
+            for (int p = 0; p < (1 << S); ++p) tu_i[s * 16 + (1 << S) - 1 + p] = neg(ipow((unsigned)p << (10 - S)));
+        int slot = 0;
+        for (int S = 4; S <= 9; ++S) {
+            const int cnt = S <= 5 ? 1 << (S - 2) : 1 << (S - 6);
+            for (int g = 0; g < cnt; ++g, ++slot)
+                for (int L = 0; L < 64; ++L) {
+                    const unsigned p = S <= 5 ? (unsigned)((L & 3) | (g << 2)) : (unsigned)(L + 64 * g);
+                    ts_i[(s * 27 + slot) * 64 + L] = neg(ipow(p << (10 - S)));
+                }
+        }
+        for (int r = 0; r < 16; ++r)
+            for (int L = 0; L < 64; ++L) {
+                const uint32_t w = ipow((unsigned)(L + 64 * r));
+                tpost[(s * 16 + r) * 64 + L] = make_uint2(w, shp(w));
+            }
+    }
+}
+
+static V4Args v4_args(const DeviceKey &key) {
+    V4Args g;
+    g.bk = key.bk_v2;
+    g.tu_f = key.tw2;
+    g.ts_f = key.tw2 + 64;
+    g.tu_i = key.tw4;
+    g.ts_i = key.tw4 + 32;
+    g.tpost = key.tw4 + 32 + 2 * 27 * 64;
+    g.qinv_neg0 = key.qinv_neg[0];
+    g.qinv_neg1 = key.qinv_neg[1];
+    g.crt_h = key.crt_h;
+    g.crt_hp = key.crt_hp;
+    return g;
+}
+
+hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    const BrInput in1 = halves > 1 ? in[1] : in[0];
+    hipLaunchKernelGGL(k_blind_rotate_v4, dim3(B * halves), dim3(kV4Threads), 0, s, v4_args(key), B, in[0], in1, mu,
+                       u_a, u_b);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, int32_t *acc, const int32_t *bara,
+                                        hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (iters < 0 || iters > kn) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_v4_debug, dim3(B), dim3(kV4Threads), 0, s, v4_args(key), iters, acc, bara);
+    return hipGetLastError();
+}
+
+}  // namespace tfhe_amd

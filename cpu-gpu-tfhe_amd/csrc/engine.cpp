@@ -74,8 +74,8 @@ int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
     if (v == 0) {
         const char *e = getenv("TFHE_AMD_BR");
-        v = e ? atoi(e) : 2;
-        if (v < 1 || v > 3) v = 2;
+        v = e ? atoi(e) : 4;
+        if (v < 1 || v > 4) v = 4;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
@@ -86,7 +86,8 @@ static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput 
     switch (br_version()) {
     case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
     case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
-    default: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
+    case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
+    default: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     }
 }
 
@@ -132,6 +133,7 @@ static int free_key(DeviceKey &k) {
     if (k.bk_ntt) (void)hipFree(k.bk_ntt);
     if (k.bk_v2) (void)hipFree(k.bk_v2);
     if (k.tw2) (void)hipFree(k.tw2);
+    if (k.tw4) (void)hipFree(k.tw4);
     if (k.ksk) (void)hipFree(k.ksk);
     if (k.tables) (void)hipFree(k.tables);
     k = DeviceKey();
@@ -189,6 +191,10 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         build_v2_twiddles(*ht, tw.data(), tw.data() + 32, tw.data() + 64, tw.data() + 64 + 2 * 27 * 64);
         HIPCHK(hipMalloc(&c->key.tw2, sizeof(uint2) * tw.size()));
         HIPCHK(hipMemcpy(c->key.tw2, tw.data(), sizeof(uint2) * tw.size(), hipMemcpyHostToDevice));
+        std::vector<uint2> tw4(kTw4Words);
+        build_v4_twiddles(*ht, tw4.data(), tw4.data() + 32, tw4.data() + 32 + 2 * 27 * 64);
+        HIPCHK(hipMalloc(&c->key.tw4, sizeof(uint2) * tw4.size()));
+        HIPCHK(hipMemcpy(c->key.tw4, tw4.data(), sizeof(uint2) * tw4.size(), hipMemcpyHostToDevice));
     }
     delete ht;
 
@@ -432,7 +438,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     const int v = br_version();
     HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
            : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
-                    : launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s));
+           : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
+                    : launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
 
@@ -535,13 +542,13 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version < 1 || br_version > 3) return TFHE_AMD_E_ARG;
+    if (br_version < 1 || br_version > 4) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }
 
 extern "C" const char *tfhe_amd_version(void) {
     static const char *names[] = {"", "tfhe_amd gfx950 ntt2x27 br-v1 ks-v2", "tfhe_amd gfx950 ntt2x27 br-v2 ks-v2",
-                                  "tfhe_amd gfx950 ntt2x27 br-v3 ks-v2"};
+                                  "tfhe_amd gfx950 ntt2x27 br-v3 ks-v2", "tfhe_amd gfx950 ntt2x27 br-v4 ks-v2"};
     return names[br_version()];
 }

@@ -13,6 +13,7 @@ struct DeviceKey {
     uint32_t *bk_ntt = nullptr;   // v1: [kn][2 primes][kKpl][2][kN], Montgomery form, 1/N folded
     uint32_t *bk_v2 = nullptr;    // v2: [kn][2 primes][2 c][kKpl][4 v][64 L][4 e] (same values)
     uint2 *tw2 = nullptr;         // v2 twiddles: uniform fwd/inv [2][16] x2, streams [2][27][64], [2][18][64]
+    uint2 *tw4 = nullptr;         // v4 inverse-CT twiddles: uniform [2][16], streams [2][27][64], post-twist [2][16][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     NttTables *tables = nullptr;  // device copy
     uint32_t qinv_neg[2] = {0, 0};
@@ -20,6 +21,7 @@ struct DeviceKey {
     bool has_bk = false;
 };
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
+constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -49,7 +51,13 @@ hipError_t launch_blind_rotate_v3(const DeviceKey &key, int B, int halves, const
                                   int32_t *u_a, int32_t *u_b, hipStream_t s);
 hipError_t launch_blind_rotate_v3_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
-// which blind-rotation kernel runs: 1, 2 or 3 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
+// v4 (v2 layout, inverse CT + lazy CRT + periodic accumulator), blind_rotate_v4.hip
+void build_v4_twiddles(const NttTables &t, uint2 *tu_i, uint2 *ts_i, uint2 *tpost);
+hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                        const int32_t *bara, hipStream_t s);
+// which blind-rotation kernel runs: 1..4 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).

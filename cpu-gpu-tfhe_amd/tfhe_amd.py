@@ -100,6 +100,11 @@ def version():
     return lib.tfhe_amd_version().decode()
 
 
+def select_kernel(generation):
+    """tfhe_amd_select_kernel: blind-rotation kernel generation 1..4 (A/B and cross-checks)."""
+    _check(lib.tfhe_amd_select_kernel(int(generation)), "select_kernel")
+
+
 def _p(a):
     if a is None:
         return None

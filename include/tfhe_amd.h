@@ -125,8 +125,9 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
 /* Select the blind-rotation kernel generation (1 = LDS radix-2 reference kernel,
- * 2 = register-resident NTT with 2 waves per ciphertext, the default, 3 = 4 waves per
- * ciphertext; env TFHE_AMD_BR=<n> does the same at startup).
+ * 2 = register-resident NTT with 2 waves per ciphertext, 3 = 4 waves per ciphertext,
+ * 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT and a periodic accumulator, the
+ * default; env TFHE_AMD_BR=<n> does the same at startup).
  * For A/B measurements and parity cross-checks; results are identical by contract. */
 int tfhe_amd_select_kernel(int br_version);
 

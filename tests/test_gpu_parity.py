@@ -118,3 +118,33 @@ def test_device_batch_1024_truth_and_sampled_parity(ctx, okey, keyset, rng):
     idx = rng.choice(B, 32, replace=False)
     o_a, o_b = okey.gate_batch("NAND", a_a[idx], a_b[idx], b_a[idx], b_b[idx])
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+
+
+def test_kernel_generations_agree(ctx, keyset, rng):
+    """Every blind-rotation generation (v1 LDS radix-2, v2, v3, v4) gives identical Torus32
+    results on the same gates and on explicit CMux steps."""
+    torch = _torch()
+    B, iters = 8, 6
+    x = rng.integers(0, 2, B)
+    y = rng.integers(0, 2, B)
+    a_a, a_b = keyset.encrypt(x, rng)
+    b_a, b_b = keyset.encrypt(y, rng)
+    acc0 = rng.integers(-2**31, 2**31, (B, 2, N), dtype=np.int64).astype(np.int32)
+    bara = rng.integers(0, 2048, (B, iters), dtype=np.int64).astype(np.int32)
+    default = T.version()
+    outs = {}
+    try:
+        for v in (1, 2, 3, 4):
+            T.select_kernel(v)
+            d_acc = torch.from_numpy(acc0.copy()).cuda()
+            ctx.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), iters)
+            ctx.sync()
+            outs[v] = (ctx.gate_host("XOR", a_a, a_b, b_a, b_b), d_acc.cpu().numpy())
+    finally:
+        T.select_kernel(int(default.split("br-v")[1][0]))
+    for v in (1, 2, 3):
+        (ra, rb), acc = outs[v]
+        (ra4, rb4), acc4 = outs[4]
+        assert np.array_equal(ra, ra4) and np.array_equal(rb, rb4), v
+        assert np.array_equal(acc, acc4), v
+    assert np.array_equal(keyset.decrypt(*outs[4][0]), x ^ y)
