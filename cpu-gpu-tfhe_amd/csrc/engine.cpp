@@ -135,6 +135,7 @@ static int free_key(DeviceKey &k) {
     if (k.tw2) (void)hipFree(k.tw2);
     if (k.tw4) (void)hipFree(k.tw4);
     if (k.ksk) (void)hipFree(k.ksk);
+    if (k.ksk4) (void)hipFree(k.ksk4);
     if (k.tables) (void)hipFree(k.tables);
     k = DeviceKey();
     return 0;
@@ -224,6 +225,9 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
                 }
         HIPCHK(hipMalloc(&c->key.ksk, sizeof(int32_t) * packed.size()));
         HIPCHK(hipMemcpy(c->key.ksk, packed.data(), sizeof(int32_t) * packed.size(), hipMemcpyHostToDevice));
+        HIPCHK(hipMalloc(&c->key.ksk4, sizeof(int32_t) * ksk_v4_words()));
+        HIPCHK(launch_ksk_to_v4(c->key.ksk, c->key.ksk4, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
     }
     return tfhe_amd_reserve(c, 64);
 }
@@ -548,7 +552,13 @@ extern "C" int tfhe_amd_select_kernel(int br_version) {
 }
 
 extern "C" const char *tfhe_amd_version(void) {
-    static const char *names[] = {"", "tfhe_amd gfx950 ntt2x27 br-v1 ks-v2", "tfhe_amd gfx950 ntt2x27 br-v2 ks-v2",
-                                  "tfhe_amd gfx950 ntt2x27 br-v3 ks-v2", "tfhe_amd gfx950 ntt2x27 br-v4 ks-v2"};
-    return names[br_version()];
+    // one immutable string per (blind-rotation, key-switch) generation pair
+    static char names[5][5][48];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int b = 1; b <= 4; b++)
+            for (int k = 1; k <= 4; k++)
+                snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
+    });
+    return names[br_version()][ks_version()];
 }

@@ -15,6 +15,7 @@ struct DeviceKey {
     uint2 *tw2 = nullptr;         // v2 twiddles: uniform fwd/inv [2][16] x2, streams [2][27][64], [2][18][64]
     uint2 *tw4 = nullptr;         // v4 inverse-CT twiddles: uniform [2][16], streams [2][27][64], post-twist [2][16][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
+    int32_t *ksk4 = nullptr;      // ks-v4: [126 column blocks][kN][kKsT][3][4]
     NttTables *tables = nullptr;  // device copy
     uint32_t qinv_neg[2] = {0, 0};
     uint32_t crt_h = 0, crt_hp = 0;
@@ -60,6 +61,10 @@ hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, 
 // which blind-rotation kernel runs: 1..4 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 
+// which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)
+int ks_version();
+size_t ksk_v4_words();
+hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s);
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).
 hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,
                             const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,

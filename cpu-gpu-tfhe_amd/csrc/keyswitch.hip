@@ -129,12 +129,213 @@ __global__ __launch_bounds__(kKsV2Threads) void k_keyswitch_v2(
     }
 }
 
+// ---------------------------------------------------------------- v3
+// v2 with the next chunk's KSK row slices prefetched into registers while the current chunk
+// is applied (12 x 16 B per thread), so the L2/MALL latency of the staging loads is hidden
+// behind the LDS gather instead of being paid once per chunk (v2 stalls at every chunk).
+constexpr int kKsLoads = kKsI * kKsT * 3 * 16 / kKsV2Threads;   // uint4 per thread per chunk = 12
+static_assert(kKsI * kKsT * 3 * 16 % kKsV2Threads == 0, "chunk must split evenly");
+
+__global__ __launch_bounds__(kKsV2Threads) void k_keyswitch_v3(
+    const int32_t *__restrict__ ksk, int B, const int32_t *__restrict__ u_a, const int32_t *__restrict__ u_b,
+    const int32_t *__restrict__ u2_a, const int32_t *__restrict__ u2_b, int32_t add_b,
+    int32_t *__restrict__ res_a, int32_t *__restrict__ res_b) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[kKsI * kKsT * 4][64];   // 64 KB
+    const int cb = blockIdx.x & 7;
+    const int ct0 = (blockIdx.x >> 3) * kKsCt;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int col = cb * 64 + lane;
+    constexpr int kPerWave = kKsCt / 4;
+    uint32_t acc[kPerWave];
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int g = ct0 + wave * kPerWave + k;
+        acc[k] = 0;
+        if (col == kn && g < B) acc[k] = (uint32_t)u_b[g] + (uint32_t)add_b + (u2_b ? (uint32_t)u2_b[g] : 0u);
+    }
+    for (int t = tid; t < kKsI * kKsT * 64; t += kKsV2Threads) rows[(t >> 6) * 4][t & 63] = 0;
+    // thread tid stages uint4 number t = tid + kKsV2Threads * l of a chunk: row t >> 4, cols 4 (t & 15)
+    uint4 pre[kKsLoads];
+    auto fetch = [&](int i0) {
+        const int32_t *src = ksk + (size_t)i0 * kKsT * 3 * kKsRow + cb * 64;
+#pragma unroll
+        for (int l = 0; l < kKsLoads; ++l) {
+            const int t = tid + kKsV2Threads * l;
+            pre[l] = *reinterpret_cast<const uint4 *>(src + (size_t)(t >> 4) * kKsRow + (t & 15) * 4);
+        }
+    };
+    fetch(0);
+    for (int i0 = 0; i0 < kN; i0 += kKsI) {
+#pragma unroll
+        for (int l = 0; l < kKsLoads; ++l) {
+            const int t = tid + kKsV2Threads * l;
+            const int row = t >> 4, c4 = (t & 15) * 4;
+            const int ij = row / 3, h = row - 3 * ij + 1;
+            *reinterpret_cast<uint4 *>(&rows[ij * 4 + h][c4]) = pre[l];
+        }
+        __syncthreads();
+        if (i0 + kKsI < kN) fetch(i0 + kKsI);        // in flight during the gather below
+#pragma unroll
+        for (int k = 0; k < kPerWave; ++k) {
+            const int g = ct0 + wave * kPerWave + k;
+            if (g >= B) break;                         // wave-uniform
+            const int32_t *ua = u_a + (size_t)g * kN + i0;
+            const int32_t *ua2 = u2_a ? u2_a + (size_t)g * kN + i0 : nullptr;
+#pragma unroll
+            for (int ii = 0; ii < kKsI; ++ii) {
+                uint32_t ab = (uint32_t)__builtin_amdgcn_readfirstlane(ua[ii]);
+                if (ua2) ab += (uint32_t)__builtin_amdgcn_readfirstlane(ua2[ii]);
+                ab += kKsPrecOffset;
+#pragma unroll
+                for (int j = 0; j < kKsT; ++j) {
+                    const uint32_t aij = (ab >> (32 - (j + 1) * kKsBasebit)) & (kKsBase - 1);
+                    acc[k] -= rows[(ii * kKsT + j) * 4 + (int)aij][lane];
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) {
+        const int g = ct0 + wave * kPerWave + k;
+        if (g >= B) break;
+        if (col < kn) res_a[(size_t)g * kn + col] = (int32_t)acc[k];
+        else if (col == kn) res_b[g] = (int32_t)acc[k];
+    }
+}
+
+// ---------------------------------------------------------------- v4
+// Lane = ciphertext.  A workgroup of 4 waves owns 256 ciphertexts and a 4-column slice of
+// the output (columns 4 cb .. 4 cb + 3; column 500 is b).  The KSK is repacked per column
+// block, [cb][i][j][h = 1..3][4] int32, so a block's slice is one contiguous 384 KB stream;
+// chunks of 32 key indices (12 KB) are double-buffered through LDS next to a resident zero
+// row (h = 0).  Each lane extracts its own digits (v_bfe) and gathers the 16-B row piece
+// with one ds_read_b128 whose base is (i, j)-constant (immediate offset): per (i, j) one
+// LDS read, 4 subtracts and 2 VALU of digit/addressing, for 64 ciphertexts at once.
+constexpr int kKs4Cols = 4;
+constexpr int kKs4Blocks = 126;                 // ceil(501 / 4)
+constexpr int kKs4I = 32;                       // key indices per chunk
+constexpr int kKs4Threads = 256;
+constexpr int kKs4ChunkU4 = kKs4I * kKsT * 3;   // uint4 pieces per chunk = 768
+static_assert(kKs4ChunkU4 % kKs4Threads == 0, "chunk must split evenly");
+
+__global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(
+    const uint4 *__restrict__ ksk4, int B, const int32_t *__restrict__ u_a, const int32_t *__restrict__ u_b,
+    const int32_t *__restrict__ u2_a, const int32_t *__restrict__ u2_b, int32_t add_b,
+    int32_t *__restrict__ res_a, int32_t *__restrict__ res_b) {
+    // buf[b][i][j][h][4 cols]: h = 0 is the zero row of lwe-keyswitch-functions.cu:919
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][kKs4I * kKsT * 4];   // 2 x 16 KB
+    // XCD-aware: workgroups with equal blockIdx % 8 stream the same column blocks
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int cb = (k & 15) * 8 + xcd;
+    const int ctg = k >> 4;
+    if (cb >= kKs4Blocks) return;                 // whole workgroup: no barrier skipped
+    const int tid = threadIdx.x;
+    const int ct = ctg * kKs4Threads + tid;
+    const bool valid = ct < B;
+    const int ctc = valid ? ct : 0;
+    for (int t = tid; t < 2 * kKs4I * kKsT; t += kKs4Threads) buf[t >> 8][(t & 255) * 4] = make_uint4(0, 0, 0, 0);
+
+    uint32_t acc[kKs4Cols];
+#pragma unroll
+    for (int c = 0; c < kKs4Cols; ++c) acc[c] = 0;
+    if (cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols && valid)
+        acc[kn - cb * kKs4Cols] = (uint32_t)u_b[ct] + (uint32_t)add_b + (u2_b ? (uint32_t)u2_b[ct] : 0u);
+
+    const uint4 *src = ksk4 + (size_t)cb * kN * kKsT * 3 + tid;
+    const uint4 *pa = reinterpret_cast<const uint4 *>(u_a + (size_t)ctc * kN);
+    const uint4 *pa2 = u2_a ? reinterpret_cast<const uint4 *>(u2_a + (size_t)ctc * kN) : nullptr;
+    // (i, j, h - 1) piece t = tid + 256 l of a chunk goes to buf[.][(t / 3) * 4 + t % 3 + 1]
+    int dst[3];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        const int t = tid + kKs4Threads * l;
+        dst[l] = (t / 3) * 4 + (t - 3 * (t / 3)) + 1;
+    }
+    // register prefetch of one chunk: 3 KSK pieces + this lane's 32 a-values (+ u2's)
+    uint4 p0 = src[0], p1 = src[kKs4Threads], p2 = src[2 * kKs4Threads];
+    uint4 av[kKs4I / 4], av2[kKs4I / 4];
+#pragma unroll
+    for (int v = 0; v < kKs4I / 4; ++v) {
+        av[v] = pa[v];
+        av2[v] = pa2 ? pa2[v] : make_uint4(0, 0, 0, 0);
+    }
+    buf[0][dst[0]] = p0; buf[0][dst[1]] = p1; buf[0][dst[2]] = p2;
+    __syncthreads();
+    for (int i0 = 0, b = 0; i0 < kN; i0 += kKs4I, b ^= 1) {
+        uint32_t a[kKs4I];
+#pragma unroll
+        for (int v = 0; v < kKs4I / 4; ++v) {
+            a[4 * v] = av[v].x + av2[v].x + kKsPrecOffset;
+            a[4 * v + 1] = av[v].y + av2[v].y + kKsPrecOffset;
+            a[4 * v + 2] = av[v].z + av2[v].z + kKsPrecOffset;
+            a[4 * v + 3] = av[v].w + av2[v].w + kKsPrecOffset;
+        }
+        const bool more = i0 + kKs4I < kN;
+        if (more) {                                          // next chunk, in flight during the gather
+            const uint4 *sn = src + (size_t)(i0 + kKs4I) * kKsT * 3;
+            p0 = sn[0]; p1 = sn[kKs4Threads]; p2 = sn[2 * kKs4Threads];
+#pragma unroll
+            for (int v = 0; v < kKs4I / 4; ++v) {
+                av[v] = pa[(i0 + kKs4I) / 4 + v];
+                if (pa2) av2[v] = pa2[(i0 + kKs4I) / 4 + v];
+            }
+        }
+        const uint4 *cur = buf[b];
+#pragma unroll
+        for (int ii = 0; ii < kKs4I; ++ii) {
+            const uint32_t ab = a[ii];
+#pragma unroll
+            for (int j = 0; j < kKsT; ++j) {
+                const uint32_t aij = (ab >> (32 - (j + 1) * kKsBasebit)) & (kKsBase - 1);
+                const uint4 r = cur[(ii * kKsT + j) * 4 + (int)aij];
+                acc[0] -= r.x; acc[1] -= r.y; acc[2] -= r.z; acc[3] -= r.w;
+            }
+            // materialise the running sums once per key index: without this LLVM re-associates
+            // the 256 subtractions of a chunk into one tree and keeps every gathered row live
+            asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+        }
+        if (more) {                                          // other buffer: last read one chunk ago
+            uint4 *nb = buf[b ^ 1];
+            nb[dst[0]] = p0; nb[dst[1]] = p1; nb[dst[2]] = p2;
+        }
+        __syncthreads();
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int c = 0; c < kKs4Cols; ++c) {
+        const int col = cb * kKs4Cols + c;
+        if (col < kn) res_a[(size_t)ct * kn + col] = (int32_t)acc[c];
+        else if (col == kn) res_b[ct] = (int32_t)acc[c];
+    }
+}
+
+// packed KSK [i][j][h - 1][kKsRow] -> v4 [cb][i][j][h - 1][4 cols]
+__global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ ksk, uint4 *__restrict__ ksk4) {
+    const size_t pieces = (size_t)kKs4Blocks * kN * kKsT * 3;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < pieces; t += (size_t)gridDim.x * 256) {
+        const int cb = (int)(t / ((size_t)kN * kKsT * 3));
+        const size_t row = t % ((size_t)kN * kKsT * 3);
+        ksk4[t] = *reinterpret_cast<const uint4 *>(ksk + row * kKsRow + cb * kKs4Cols);
+    }
+}
+
 }  // namespace
+
+size_t ksk_v4_words() { return (size_t)kKs4Blocks * kN * kKsT * 3 * 4; }
+
+hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s) {
+    hipLaunchKernelGGL(k_ksk_to_v4, dim3(2048), dim3(256), 0, s, d_ksk, reinterpret_cast<uint4 *>(d_ksk4));
+    return hipGetLastError();
+}
 
 int ks_version() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_KS");
-        return (e && atoi(e) == 1) ? 1 : 2;
+        const int x = e ? atoi(e) : 4;
+        return (x >= 1 && x <= 4) ? x : 4;
     }();
     return v;
 }
@@ -146,10 +347,18 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
     if (ks_version() == 1) {
         hipLaunchKernelGGL(k_keyswitch_v1, dim3(B), dim3(kKsThreads), 0, s, key.ksk, u_a, u_b, u2_a, u2_b,
                            add_b, res_a, res_b);
-    } else {
+    } else if (ks_version() == 2) {
         const int blocks = ((B + kKsCt - 1) / kKsCt) * 8;
         hipLaunchKernelGGL(k_keyswitch_v2, dim3(blocks), dim3(kKsV2Threads), 0, s, key.ksk, B, u_a, u_b, u2_a,
                            u2_b, add_b, res_a, res_b);
+    } else if (ks_version() == 3) {
+        const int blocks = ((B + kKsCt - 1) / kKsCt) * 8;
+        hipLaunchKernelGGL(k_keyswitch_v3, dim3(blocks), dim3(kKsV2Threads), 0, s, key.ksk, B, u_a, u_b, u2_a,
+                           u2_b, add_b, res_a, res_b);
+    } else {
+        const int groups = (B + kKs4Threads - 1) / kKs4Threads;
+        hipLaunchKernelGGL(k_keyswitch_v4, dim3(128 * groups), dim3(kKs4Threads), 0, s,
+                           reinterpret_cast<const uint4 *>(key.ksk4), B, u_a, u_b, u2_a, u2_b, add_b, res_a, res_b);
     }
     return hipGetLastError();
 }
