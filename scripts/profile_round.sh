@@ -1,0 +1,26 @@
+#!/usr/bin/env bash
+# Runs on the GPU box (gpurun): rocprofv3 kernel trace/stats of the default bench, then the
+# PMC passes (FETCH_SIZE, WRITE_SIZE, SQ counters) each in its own run, kernel-trace only.
+#   bash scripts/profile_round.sh <tag> [batch]
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1
+BATCH=${2:-1024}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH="$R/bench.py --steps 5 --warmup 1 --batch $BATCH --no-cpu-baseline"
+run() {   # name, extra rocprofv3 args...
+  local name=$1; shift
+  timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
+run trace --kernel-trace --stats
+run fetch --kernel-trace --pmc FETCH_SIZE
+run write --kernel-trace --pmc WRITE_SIZE
+run sq --kernel-trace --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY
+run sq2 --kernel-trace --pmc SQ_INSTS_LDS SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_WAVES
+exit 0
