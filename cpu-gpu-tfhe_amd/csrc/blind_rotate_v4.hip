@@ -143,27 +143,30 @@ __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, in
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int B, BrInput in0, BrInput in1,
-                                                                int32_t mu, int32_t *__restrict__ u_a,
-                                                                int32_t *__restrict__ u_b) {
-    __shared__ V4Shared sh;
+// The linear combination x = (0, c) + sa X + sb Y + sc Z that feeds one blind rotation
+// (gate prologues boot-gates.cu:98-448; a circuit row adds a third input for MAJ / XOR3).
+struct RowTerms {
+    int32_t c, sa, sb, sc;
+    const int32_t *xa, *xb, *ya, *yb, *za, *zb;   // a rows (kn) and b words; y/z may be null
+};
+
+// prologue + modswitch + 500 CMux steps + extraction of one ciphertext into (ua, *ub)
+__device__ __forceinline__ void br_v4_body(V4Shared &sh, const V4Args &g, const RowTerms &t, int32_t mu,
+                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub) {
     const int tid = threadIdx.x;
     const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
-    const int gct = blockIdx.x;
-    const int half = gct >= B;
-    const int idx = half ? gct - B : gct;
-    const BrInput &in = half ? in1 : in0;
-
-    // gate prologue + modulus switching (boot-gates.cu:98-397; lwe-bootstrapping-functions-fft.cu:1851-1858)
+    // gate prologue + modulus switching (lwe-bootstrapping-functions-fft.cu:1851-1858)
     for (int i = tid; i < kn; i += kV4Threads) {
-        uint32_t x = (uint32_t)in.sa * (uint32_t)in.x_a[(size_t)idx * kn + i];
-        if (in.sb) x += (uint32_t)in.sb * (uint32_t)in.y_a[(size_t)idx * kn + i];
+        uint32_t x = t.xa ? (uint32_t)t.sa * (uint32_t)t.xa[i] : 0u;
+        if (t.ya) x += (uint32_t)t.sb * (uint32_t)t.ya[i];
+        if (t.za) x += (uint32_t)t.sc * (uint32_t)t.za[i];
         sh.bara[i] = modswitch_2N(x);
     }
     if (tid == 0) {
-        uint32_t xb = (uint32_t)in.c + (uint32_t)in.sa * (uint32_t)in.x_b[idx];
-        if (in.sb) xb += (uint32_t)in.sb * (uint32_t)in.y_b[idx];
+        uint32_t xb = (uint32_t)t.c + (t.xb ? (uint32_t)t.sa * (uint32_t)t.xb[0] : 0u);
+        if (t.yb) xb += (uint32_t)t.sb * (uint32_t)t.yb[0];
+        if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
     __syncthreads();
@@ -181,9 +184,50 @@ __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int
         cmux_v4(sh, g, i, a, s, L);
     }
     // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
-    int32_t *ua = u_a + (size_t)gct * kN;
     for (int j = tid; j < kN; j += kV4Threads) ua[j] = (int32_t)sh.E[0][(k2N - j) & (k2N - 1)];
-    if (tid == 0) u_b[gct] = (int32_t)sh.E[1][0];
+    if (tid == 0) *ub = (int32_t)sh.E[1][0];
+}
+
+// gate batch: ciphertext gct of half h = gct / B reads in_h at index gct mod B
+__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int B, BrInput in0, BrInput in1,
+                                                                int32_t mu, int32_t *__restrict__ u_a,
+                                                                int32_t *__restrict__ u_b) {
+    __shared__ V4Shared sh;
+    const int gct = blockIdx.x;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+    RowTerms t;
+    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+    t.za = nullptr; t.zb = nullptr;
+    br_v4_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+}
+
+// circuit level: blockIdx.x = instance k < B, blockIdx.y = row r; wires are [W][B] ciphertexts,
+// the extracted sample of (r, k) goes to u slot r B + k
+__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_rows(V4Args g, int B, const CircRow *__restrict__ rows,
+                                                                     const int32_t *__restrict__ wa,
+                                                                     const int32_t *__restrict__ wb, int32_t mu,
+                                                                     int32_t *__restrict__ u_a,
+                                                                     int32_t *__restrict__ u_b) {
+    __shared__ V4Shared sh;
+    const int k = blockIdx.x, r = blockIdx.y;
+    const CircRow row = rows[r];
+    auto wire = [&](int w, const int32_t *&pa, const int32_t *&pb) {
+        if (w < 0) { pa = nullptr; pb = nullptr; return; }
+        const size_t slot = (size_t)w * B + k;
+        pa = wa + slot * kn;
+        pb = wb + slot;
+    };
+    RowTerms t;
+    t.c = row.c; t.sa = row.sa; t.sb = row.sb; t.sc = row.sc;
+    wire(row.x, t.xa, t.xb);
+    wire(row.y, t.ya, t.yb);
+    wire(row.z, t.za, t.zb);
+    const size_t slot = (size_t)r * B + k;
+    br_v4_body(sh, g, t, mu, u_a + slot * kN, u_b + slot);
 }
 
 __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_debug(V4Args g, int iters, int32_t *__restrict__ acc,
@@ -261,6 +305,15 @@ hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const
     const BrInput in1 = halves > 1 ? in[1] : in[0];
     hipLaunchKernelGGL(k_blind_rotate_v4, dim3(B * halves), dim3(kV4Threads), 0, s, v4_args(key), B, in[0], in1, mu,
                        u_a, u_b);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    if (B <= 0 || nrows <= 0) return hipSuccess;
+    if (nrows > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_v4_rows, dim3(B, nrows), dim3(kV4Threads), 0, s, v4_args(key), B, rows, wa, wb,
+                       mu, u_a, u_b);
     return hipGetLastError();
 }
 

@@ -1,0 +1,474 @@
+// circuit.cpp — batched circuit schedules over the MI355X engine.
+//
+// The reference evaluates Cipher's integer operations (cpuParallel/Cipher.cpp:83-392) one
+// synchronous gate at a time, and its GPU path batches hand-written gate groups
+// (taskLevelParallelAdd_bitwise gpuParallel/main.cu:821-890, the compound ANDXOR / XORXOR
+// gates boot-gates.cu:3027-3098, multiplyLweSamples main.cu:1483-1579).  Here a circuit is a
+// DAG of gates over SSA wires; the compiler levels it by bootstrap depth and every level runs
+// as ONE blind-rotation launch over all of its gates x B independent instances plus ONE key
+// switch launch, so any circuit gets the batching the reference wrote by hand for two.
+//
+// Bootstrap-free gates (NOT, COPY, CONSTANT; boot-gates.cu:242-267) become affine forms
+// (0, c) + s W[base] that are folded into the rows that consume them and also materialised
+// in the wire array.  Three-input rows give MAJ and XOR3 in one bootstrap each, so a
+// full adder is one level (2 bootstraps) instead of the reference's three (5 bootstraps).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "engine.h"
+#include "../../include/tfhe_amd.h"
+
+using namespace tfhe_amd;
+
+namespace {
+
+constexpr int32_t kE8 = 1 << 29;   // modSwitchToTorus32(1, 8)
+constexpr int32_t kE4 = 1 << 30;   // modSwitchToTorus32(1, 4)
+
+struct Node {
+    int kind;            // 0 = input, 1 = bootstrapped row(s), 2 = affine (no bootstrap)
+    int gate;            // TFHE_GATE_* (kind 1, 2) or -1
+    int32_t c0;          // lincomb / affine constant
+    int32_t s[3];        // lincomb coefficients
+    int in[3];           // input wires (-1 = absent)
+};
+
+struct Affine {          // W = (0, c) + s W[base]; base = -1: the trivial sample (0, c)
+    int32_t c, s;
+    int base;
+};
+
+}  // namespace
+
+struct TfheAmdCircuit {
+    std::vector<Node> nodes;           // one per wire
+    // compiled schedule
+    bool compiled = false;
+    struct Level { int row0, nrows, ks0, nks, lin0, nlin; };
+    std::vector<Level> levels;         // levels[0]: affine nodes over inputs only
+    std::vector<CircRow> rows;
+    std::vector<CircKs> ks;
+    std::vector<CircLin> lin;
+    int n_boot = 0, max_rows = 0;
+    // device copies (per device) and u scratch
+    int dev = -1;
+    void *d_tab = nullptr;
+    int32_t *u_a = nullptr, *u_b = nullptr;
+    size_t u_slots = 0;
+    ~TfheAmdCircuit() { release(); }
+    void release() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+        if (d_tab) (void)hipFree(d_tab);
+        if (u_a) (void)hipFree(u_a);
+        if (u_b) (void)hipFree(u_b);
+        d_tab = nullptr; u_a = nullptr; u_b = nullptr; u_slots = 0; dev = -1;
+    }
+};
+
+namespace {
+
+bool row_spec(int gate, int32_t *c, int32_t *s0, int32_t *s1, int32_t *s2) {
+    // boot-gates.cu:98-397 constants; MAJ / XOR3: circuit rows of this engine
+    *s2 = 0;
+    switch (gate) {
+    case TFHE_GATE_NAND:  *c = kE8;  *s0 = -1; *s1 = -1; return true;
+    case TFHE_GATE_OR:    *c = kE8;  *s0 = 1;  *s1 = 1;  return true;
+    case TFHE_GATE_AND:   *c = -kE8; *s0 = 1;  *s1 = 1;  return true;
+    case TFHE_GATE_XOR:   *c = kE4;  *s0 = 2;  *s1 = 2;  return true;
+    case TFHE_GATE_XNOR:  *c = -kE4; *s0 = -2; *s1 = -2; return true;
+    case TFHE_GATE_NOR:   *c = -kE8; *s0 = -1; *s1 = -1; return true;
+    case TFHE_GATE_ANDNY: *c = -kE8; *s0 = -1; *s1 = 1;  return true;
+    case TFHE_GATE_ANDYN: *c = -kE8; *s0 = 1;  *s1 = -1; return true;
+    case TFHE_GATE_ORNY:  *c = kE8;  *s0 = -1; *s1 = 1;  return true;
+    case TFHE_GATE_ORYN:  *c = kE8;  *s0 = 1;  *s1 = -1; return true;
+    // majority: a + b + c in {+-1/8, +-3/8}, positive iff at least two inputs are 1
+    case TFHE_GATE_MAJ:   *c = 0;    *s0 = 1;  *s1 = 1;  *s2 = 1; return true;
+    // parity: 2(a + b + c) is -1/4 (mod 1) for an odd number of ones and +1/4 for an even one
+    case TFHE_GATE_XOR3:  *c = 0;    *s0 = -2; *s1 = -2; *s2 = -2; return true;
+    default: return false;
+    }
+}
+
+int n_inputs(int gate) {
+    switch (gate) {
+    case TFHE_GATE_MUX: case TFHE_GATE_MAJ: case TFHE_GATE_XOR3: return 3;
+    case TFHE_GATE_NOT: case TFHE_GATE_COPY: return 1;
+    case TFHE_GATE_CONST: return 0;
+    default: return 2;
+    }
+}
+
+// row = (0, c0) + sum_t coef_t * A_t with A_t affine: fold constants, merge equal bases
+bool build_row(int32_t c0, const int32_t *coef, const Affine *A, int n, CircRow *row) {
+    int32_t c = c0;
+    int base[3] = {-1, -1, -1};
+    int32_t s[3] = {0, 0, 0};
+    int m = 0;
+    for (int t = 0; t < n; ++t) {
+        if (coef[t] == 0) continue;
+        c = (int32_t)((uint32_t)c + (uint32_t)coef[t] * (uint32_t)A[t].c);
+        if (A[t].base < 0 || A[t].s == 0) continue;
+        const int32_t k = (int32_t)((uint32_t)coef[t] * (uint32_t)A[t].s);
+        int u = 0;
+        while (u < m && base[u] != A[t].base) ++u;
+        if (u == m) { base[m] = A[t].base; s[m] = 0; ++m; }
+        s[u] = (int32_t)((uint32_t)s[u] + (uint32_t)k);
+    }
+    *row = CircRow{c, s[0], s[1], s[2], base[0], base[1], base[2], 0};
+    return true;
+}
+
+int compile(TfheAmdCircuit *C) {
+    const int W = (int)C->nodes.size();
+    std::vector<Affine> aff(W);
+    std::vector<int> level(W, 0);
+    // per level buckets (index 0 = affine over inputs / constants only)
+    std::vector<std::vector<CircRow>> rows;
+    std::vector<std::vector<CircKs>> kss;
+    std::vector<std::vector<CircLin>> lins;
+    auto ensure = [&](int L) {
+        if ((int)rows.size() <= L) { rows.resize(L + 1); kss.resize(L + 1); lins.resize(L + 1); }
+    };
+    ensure(0);
+    C->n_boot = 0;
+    for (int w = 0; w < W; ++w) {
+        const Node &nd = C->nodes[w];
+        if (nd.kind == 0) { aff[w] = Affine{0, 1, w}; level[w] = 0; continue; }
+        for (int t = 0; t < 3; ++t)
+            if (nd.in[t] >= w) return TFHE_AMD_E_ARG;       // SSA order: inputs defined earlier
+        if (nd.kind == 2) {
+            Affine a;
+            if (nd.gate == TFHE_GATE_CONST) a = Affine{nd.c0, 0, -1};
+            else {
+                const Affine &x = aff[nd.in[0]];
+                const int32_t sg = nd.gate == TFHE_GATE_NOT ? -1 : 1;
+                a = Affine{(int32_t)((uint32_t)sg * (uint32_t)x.c), (int32_t)((uint32_t)sg * (uint32_t)x.s), x.base};
+            }
+            aff[w] = a;
+            level[w] = a.base < 0 ? 0 : level[a.base];
+            ensure(level[w]);
+            lins[level[w]].push_back(CircLin{a.c, a.s, a.base, w});
+            continue;
+        }
+        // bootstrapped
+        Affine A[3];
+        int L = 0;
+        for (int t = 0; t < 3; ++t) {
+            if (nd.in[t] < 0) { A[t] = Affine{0, 0, -1}; continue; }
+            A[t] = aff[nd.in[t]];
+            if (A[t].base >= 0) L = std::max(L, level[A[t].base]);
+        }
+        L += 1;
+        ensure(L);
+        level[w] = L;
+        aff[w] = Affine{0, 1, w};
+        auto &R = rows[L];
+        if (nd.gate == TFHE_GATE_MUX) {
+            // boot-gates.cu:407-448: u1 = woKS(-1/8 + a + b), u2 = woKS(-1/8 - a + c),
+            // W = KS((0, 1/8) + u1 + u2)
+            const int32_t k1[2] = {1, 1}, k2[2] = {-1, 1};
+            const Affine a1[2] = {A[0], A[1]}, a2[2] = {A[0], A[2]};
+            CircRow r1, r2;
+            build_row(-kE8, k1, a1, 2, &r1);
+            build_row(-kE8, k2, a2, 2, &r2);
+            R.push_back(r1);
+            R.push_back(r2);
+            kss[L].push_back(CircKs{(int)R.size() - 2, (int)R.size() - 1, kE8, w});
+            C->n_boot += 2;
+        } else {
+            CircRow r;
+            build_row(nd.c0, nd.s, A, 3, &r);
+            R.push_back(r);
+            kss[L].push_back(CircKs{(int)R.size() - 1, -1, 0, w});
+            C->n_boot += 1;
+        }
+    }
+    C->levels.clear(); C->rows.clear(); C->ks.clear(); C->lin.clear();
+    C->max_rows = 0;
+    for (size_t L = 0; L < rows.size(); ++L) {
+        TfheAmdCircuit::Level lv{(int)C->rows.size(), (int)rows[L].size(), (int)C->ks.size(), (int)kss[L].size(),
+                                 (int)C->lin.size(), (int)lins[L].size()};
+        if (lv.nrows > 65535) return TFHE_AMD_E_ARG;
+        C->rows.insert(C->rows.end(), rows[L].begin(), rows[L].end());
+        C->ks.insert(C->ks.end(), kss[L].begin(), kss[L].end());
+        C->lin.insert(C->lin.end(), lins[L].begin(), lins[L].end());
+        C->levels.push_back(lv);
+        C->max_rows = std::max(C->max_rows, lv.nrows);
+    }
+    C->compiled = true;
+    return TFHE_AMD_OK;
+}
+
+int add_node(TfheAmdCircuit *C, const Node &n) {
+    const int w = (int)C->nodes.size();
+    for (int t = 0; t < 3; ++t)
+        if (n.in[t] < -1 || n.in[t] >= w) return TFHE_AMD_E_ARG;
+    C->nodes.push_back(n);
+    C->compiled = false;
+    return w;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+
+extern "C" int tfhe_amd_circuit_create(TfheAmdCircuit **out) {
+    if (!out) return TFHE_AMD_E_ARG;
+    *out = new TfheAmdCircuit();
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_circuit_destroy(TfheAmdCircuit *c) {
+    delete c;
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_circuit_inputs(TfheAmdCircuit *c, int count) {
+    if (!c || count < 0) return TFHE_AMD_E_ARG;
+    const int first = (int)c->nodes.size();
+    for (int i = 0; i < count; ++i) c->nodes.push_back(Node{0, -1, 0, {0, 0, 0}, {-1, -1, -1}});
+    c->compiled = false;
+    return first;
+}
+
+extern "C" int tfhe_amd_circuit_gate(TfheAmdCircuit *c, int gate, int a, int b, int cc) {
+    if (!c) return TFHE_AMD_E_ARG;
+    const int ni = n_inputs(gate);
+    const int in[3] = {ni > 0 ? a : -1, ni > 1 ? b : -1, ni > 2 ? cc : -1};
+    for (int t = 0; t < ni; ++t)
+        if (in[t] < 0) return TFHE_AMD_E_ARG;
+    Node n{1, gate, 0, {0, 0, 0}, {in[0], in[1], in[2]}};
+    if (gate == TFHE_GATE_NOT || gate == TFHE_GATE_COPY) n.kind = 2;
+    else if (gate == TFHE_GATE_CONST) { n.kind = 2; n.c0 = a ? kE8 : -kE8; n.in[0] = -1; }
+    else if (gate != TFHE_GATE_MUX && !row_spec(gate, &n.c0, &n.s[0], &n.s[1], &n.s[2])) return TFHE_AMD_E_ARG;
+    return add_node(c, n);
+}
+
+extern "C" int tfhe_amd_circuit_lincomb(TfheAmdCircuit *c, int32_t c0, int32_t sa, int a, int32_t sb, int b,
+                                        int32_t sc, int cc) {
+    if (!c || a < 0) return TFHE_AMD_E_ARG;
+    Node n{1, -1, c0, {sa, b >= 0 ? sb : 0, cc >= 0 ? sc : 0}, {a, b, cc}};
+    return add_node(c, n);
+}
+
+extern "C" int tfhe_amd_circuit_node(const TfheAmdCircuit *c, int w, int *kind, int *gate, int32_t *c0, int32_t *s,
+                                     int *in) {
+    if (!c || w < 0 || w >= (int)c->nodes.size()) return TFHE_AMD_E_ARG;
+    const Node &n = c->nodes[w];
+    if (kind) *kind = n.kind;
+    if (gate) *gate = n.gate;
+    if (c0) *c0 = n.c0;
+    for (int t = 0; t < 3; ++t) {
+        if (s) s[t] = n.s[t];
+        if (in) in[t] = n.in[t];
+    }
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_circuit_info(TfheAmdCircuit *c, int *n_wires, int *n_gates, int *n_bootstraps,
+                                     int *depth) {
+    if (!c) return TFHE_AMD_E_ARG;
+    if (!c->compiled) {
+        const int rc = compile(c);
+        if (rc != TFHE_AMD_OK) return rc;
+    }
+    int ng = 0;
+    for (const Node &n : c->nodes) ng += n.kind != 0;
+    if (n_wires) *n_wires = (int)c->nodes.size();
+    if (n_gates) *n_gates = ng;
+    if (n_bootstraps) *n_bootstraps = c->n_boot;
+    if (depth) *depth = (int)c->levels.size() - 1;
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_level, int cap) {
+    if (!c) return TFHE_AMD_E_ARG;
+    if (!c->compiled) {
+        const int rc = compile(c);
+        if (rc != TFHE_AMD_OK) return rc;
+    }
+    const int nl = (int)c->levels.size();
+    for (int L = 0; L < nl && L < cap; ++L) rows_per_level[L] = c->levels[L].nrows;
+    return nl;
+}
+
+// wires_a [n_wires][B][500], wires_b [n_wires][B] on the context's device; input wires filled
+int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
+                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb) {
+    if (!c->compiled) {
+        const int rc = compile(c);
+        if (rc != TFHE_AMD_OK) return rc;
+    }
+    (void)ctx;
+    if (c->dev != device || !c->d_tab) {
+        c->release();
+        c->dev = device;
+        const size_t bytes = sizeof(CircRow) * c->rows.size() + sizeof(CircKs) * c->ks.size() +
+                             sizeof(CircLin) * c->lin.size() + 64;
+        if (hipMalloc(&c->d_tab, bytes) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        char *p = (char *)c->d_tab;
+        if (!c->rows.empty() && hipMemcpy(p, c->rows.data(), sizeof(CircRow) * c->rows.size(),
+                                          hipMemcpyHostToDevice) != hipSuccess) return TFHE_AMD_E_HIP;
+        p += sizeof(CircRow) * c->rows.size();
+        if (!c->ks.empty() && hipMemcpy(p, c->ks.data(), sizeof(CircKs) * c->ks.size(),
+                                        hipMemcpyHostToDevice) != hipSuccess) return TFHE_AMD_E_HIP;
+        p += sizeof(CircKs) * c->ks.size();
+        if (!c->lin.empty() && hipMemcpy(p, c->lin.data(), sizeof(CircLin) * c->lin.size(),
+                                         hipMemcpyHostToDevice) != hipSuccess) return TFHE_AMD_E_HIP;
+    }
+    const size_t need = (size_t)c->max_rows * B;
+    if (need > c->u_slots) {
+        if (c->u_a) (void)hipFree(c->u_a);
+        if (c->u_b) (void)hipFree(c->u_b);
+        c->u_a = nullptr; c->u_b = nullptr; c->u_slots = 0;
+        if (hipMalloc(&c->u_a, sizeof(int32_t) * kN * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        if (hipMalloc(&c->u_b, sizeof(int32_t) * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        c->u_slots = need;
+    }
+    const CircRow *d_rows = (const CircRow *)c->d_tab;
+    const CircKs *d_ks = (const CircKs *)(d_rows + c->rows.size());
+    const CircLin *d_lin = (const CircLin *)(d_ks + c->ks.size());
+    for (const auto &lv : c->levels) {
+        if (lv.nrows) {
+            if (launch_blind_rotate_v4_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s) !=
+                hipSuccess) return TFHE_AMD_E_HIP;
+            if (launch_keyswitch_rows(key, B, lv.nks, d_ks + lv.ks0, c->u_a, c->u_b, wa, wb, s) != hipSuccess)
+                return TFHE_AMD_E_HIP;
+        }
+        if (lv.nlin && launch_circuit_linear(B, lv.nlin, d_lin + lv.lin0, wa, wb, s) != hipSuccess)
+            return TFHE_AMD_E_HIP;
+    }
+    return TFHE_AMD_OK;
+}
+
+// ------------------------------------------------------------------ integer builders
+// Little-endian bit vectors of wire ids (bit 0 first), as Cipher.cpp stores its LweSample
+// arrays.  Each builder returns a status; results are written to caller arrays.
+
+namespace {
+
+int G(TfheAmdCircuit *c, int gate, int a, int b = -1, int cc = -1) { return tfhe_amd_circuit_gate(c, gate, a, b, cc); }
+
+// full adder: one level (XOR3 and MAJ side by side); cin may be -1 (zero)
+void full_add(TfheAmdCircuit *c, int a, int b, int cin, int *s, int *cout) {
+    if (cin < 0) {
+        *s = G(c, TFHE_GATE_XOR, a, b);
+        *cout = G(c, TFHE_GATE_AND, a, b);
+    } else {
+        *s = G(c, TFHE_GATE_XOR3, a, b, cin);
+        *cout = G(c, TFHE_GATE_MAJ, a, b, cin);
+    }
+}
+
+}  // namespace
+
+// ripple-carry adder: sum[i] = a[i] ^ b[i] ^ c_i, c_{i+1} = MAJ(a[i], b[i], c_i)
+// (Cipher::add / operator+, Cipher.cpp:237-276; main.cu:821-890).  Returns the carry-out wire.
+extern "C" int tfhe_amd_circuit_add(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int carry_in,
+                                    int *sum) {
+    if (!c || nbits <= 0 || !a || !b || !sum) return TFHE_AMD_E_ARG;
+    int carry = carry_in;
+    for (int i = 0; i < nbits; ++i) {
+        int s, co;
+        full_add(c, a[i], b[i], carry, &s, &co);
+        if (s < 0 || co < 0) return TFHE_AMD_E_ARG;
+        sum[i] = s;
+        carry = co;
+    }
+    return carry;
+}
+
+// a - b = a + ~b + 1 (operator-, Cipher.cpp:232-235 via twosComplement); returns the carry-out
+extern "C" int tfhe_amd_circuit_sub(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *diff) {
+    if (!c || nbits <= 0 || !a || !b || !diff) return TFHE_AMD_E_ARG;
+    std::vector<int> nb(nbits);
+    for (int i = 0; i < nbits; ++i) nb[i] = G(c, TFHE_GATE_NOT, b[i]);
+    const int one = G(c, TFHE_GATE_CONST, 1);
+    return tfhe_amd_circuit_add(c, nbits, a, nb.data(), one, diff);
+}
+
+// parallel-prefix (Sklansky) adder: depth 2 + log2(nbits).  Group generate/propagate
+// combine (G, P) o (G', P') = (G | (P & G'), P & P'): with G, P exclusive (p = a ^ b),
+// G | (P & G') is one threshold bootstrap: 2G + P + G' - 3/8 (as +-1/8 inputs: c = +1/8).
+extern "C" int tfhe_amd_circuit_add_prefix(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *sum) {
+    if (!c || nbits <= 0 || !a || !b || !sum) return TFHE_AMD_E_ARG;
+    std::vector<int> g(nbits), p(nbits), G_(nbits), P_(nbits);
+    for (int i = 0; i < nbits; ++i) {
+        g[i] = G(c, TFHE_GATE_AND, a[i], b[i]);
+        p[i] = G(c, TFHE_GATE_XOR, a[i], b[i]);
+    }
+    G_ = g;
+    P_ = p;
+    for (int d = 1; d < nbits; d <<= 1) {
+        std::vector<int> Gn = G_, Pn = P_;
+        for (int i = 0; i < nbits; ++i) {
+            if (!(i & d)) continue;
+            const int j = (i & ~(d - 1)) - 1;     // Sklansky: combine with the top of the lower block
+            Gn[i] = tfhe_amd_circuit_lincomb(c, kE8, 2, G_[i], 1, P_[i], 1, G_[j]);
+            Pn[i] = G(c, TFHE_GATE_AND, P_[i], P_[j]);
+        }
+        G_ = Gn;
+        P_ = Pn;
+    }
+    sum[0] = p[0];
+    for (int i = 1; i < nbits; ++i) sum[i] = G(c, TFHE_GATE_XOR, p[i], G_[i - 1]);
+    return G_[nbits - 1];
+}
+
+// unsigned n x n -> 2n multiplier: n^2 partial products (one level of ANDs, the reference's
+// bootsAND over iBits^2, main.cu:1506-1528), a Dadda carry-save tree (one level per stage:
+// full adders = XOR3 + MAJ, half adders = XOR + AND, target heights 2, 3, 4, 6, 9, 13, ...),
+// then a parallel-prefix adder for the last two rows.  Depth 1 + stages + 2 + log2(2n).
+extern "C" int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *prod) {
+    if (!c || nbits <= 0 || !a || !b || !prod) return TFHE_AMD_E_ARG;
+    const int W = 2 * nbits;
+    std::vector<std::vector<int>> col(W);
+    for (int i = 0; i < nbits; ++i)
+        for (int j = 0; j < nbits; ++j) col[i + j].push_back(G(c, TFHE_GATE_AND, a[j], b[i]));
+    std::vector<int> targets{2};
+    while (targets.back() < nbits) targets.push_back(targets.back() * 3 / 2);
+    for (int st = (int)targets.size() - 1; st >= 0; --st) {
+        const int d = targets[st];
+        size_t hmax = 0;
+        for (auto &v : col) hmax = std::max(hmax, v.size());
+        if ((int)hmax <= d) continue;
+        std::vector<std::vector<int>> nx(W);
+        for (int k = 0; k < W; ++k) {
+            auto &v = col[k];
+            const int cin = (int)nx[k].size();     // carries already produced into k this stage
+            int h = (int)v.size();
+            size_t t = 0;
+            while (h + cin > d) {
+                int s, co;
+                if (h + cin - d >= 2 && t + 3 <= v.size()) {
+                    full_add(c, v[t], v[t + 1], v[t + 2], &s, &co);
+                    t += 3;
+                    h -= 2;
+                } else {
+                    s = G(c, TFHE_GATE_XOR, v[t], v[t + 1]);
+                    co = G(c, TFHE_GATE_AND, v[t], v[t + 1]);
+                    t += 2;
+                    h -= 1;
+                }
+                nx[k].push_back(s);
+                if (k + 1 < W) nx[k + 1].push_back(co);
+            }
+            for (; t < v.size(); ++t) nx[k].push_back(v[t]);
+        }
+        col.swap(nx);
+    }
+    // two rows (missing bits = constant 0)
+    int zero = -1;
+    std::vector<int> x(W), y(W);
+    for (int k = 0; k < W; ++k) {
+        if (col[k].size() < 2 && zero < 0) zero = G(c, TFHE_GATE_CONST, 0);
+        x[k] = col[k].size() > 0 ? col[k][0] : zero;
+        y[k] = col[k].size() > 1 ? col[k][1] : zero;
+    }
+    tfhe_amd_circuit_add_prefix(c, W, x.data(), y.data(), prod);
+    return TFHE_AMD_OK;
+}

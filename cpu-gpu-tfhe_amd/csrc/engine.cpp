@@ -545,6 +545,21 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
     return c;
 }
 
+// circuit.cpp
+int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
+                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb);
+
+extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ, int B, int32_t *wires_a,
+                                        int32_t *wires_b, void *stream) {
+    if (!c || !circ || B < 0 || !c->key.has_bk || !c->key.ksk4) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!wires_a || !wires_b) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    std::lock_guard<std::mutex> lk(c->mu);
+    return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b);
+}
+
 extern "C" int tfhe_amd_select_kernel(int br_version) {
     if (br_version < 1 || br_version > 4) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);

@@ -31,6 +31,21 @@ struct BrInput {
     int32_t c, sa, sb;
 };
 
+// One bootstrapped row of a circuit level (circuit.cpp): the blind rotation input is
+// (0, c) + sa W[x] + sb W[y] + sc W[z] over wire indices (-1 = absent; x is always present).
+struct CircRow {
+    int32_t c, sa, sb, sc;
+    int32_t x, y, z, pad;
+};
+// One key-switched circuit output: W[out] = KS(u[r1] (+ u[r2] if r2 >= 0) + (0, add_b)).
+struct CircKs {
+    int32_t r1, r2, add_b, out;
+};
+// One bootstrap-free node: W[out] = (0, c) + s W[in]   (in = -1: the trivial sample (0, c)).
+struct CircLin {
+    int32_t c, s, in, out;
+};
+
 // BK conversion (coefficient -> NTT domain) on the device; d_bk_coef = [kn][4][2][kN]
 hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const NttTables *d_tab,
                             hipStream_t s);
@@ -58,12 +73,20 @@ hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const
                                   int32_t *u_a, int32_t *u_b, hipStream_t s);
 hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
+// circuit level (v4 kernel): B instances x nrows rows, wires [W][B] ciphertexts, u slots r B + k
+hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
 // which blind-rotation kernel runs: 1..4 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 
 // which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)
 int ks_version();
 size_t ksk_v4_words();
+// circuit level key switch: nks outputs x B instances; lane t = g B + k
+hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const CircKs *ks, const int32_t *u_a,
+                                 const int32_t *u_b, int32_t *wa, int32_t *wb, hipStream_t s);
+// bootstrap-free nodes: nlin x B instances
+hipError_t launch_circuit_linear(int B, int nlin, const CircLin *lin, int32_t *wa, int32_t *wb, hipStream_t s);
 hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s);
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).
 hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,

@@ -16,6 +16,7 @@
 #include "engine.h"
 #include "modarith.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace tfhe_amd {
@@ -221,10 +222,55 @@ constexpr int kKs4Threads = 256;
 constexpr int kKs4ChunkU4 = kKs4I * kKsT * 3;   // uint4 pieces per chunk = 768
 static_assert(kKs4ChunkU4 % kKs4Threads == 0, "chunk must split evenly");
 
-__global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(
-    const uint4 *__restrict__ ksk4, int B, const int32_t *__restrict__ u_a, const int32_t *__restrict__ u_b,
-    const int32_t *__restrict__ u2_a, const int32_t *__restrict__ u2_b, int32_t add_b,
-    int32_t *__restrict__ res_a, int32_t *__restrict__ res_b) {
+// Where lane ct of the key switch reads and writes (gate batches and circuit levels).
+struct KsLane {
+    const int32_t *ua, *ua2;   // extracted sample(s), kN words each; ua2 may be null
+    uint32_t b;                // u_b (+ u2_b) + add_b
+    int32_t *ra, *rb;          // result row (kn words) and b word
+};
+struct KsPlain {               // gate batch: u[ct] (+ u2[ct]) + (0, add_b) -> res[ct]
+    const int32_t *u_a, *u_b, *u2_a, *u2_b;
+    int32_t add_b;
+    int32_t *res_a, *res_b;
+    int B;
+    __device__ int count() const { return B; }
+    __device__ KsLane lane(int ct) const {
+        KsLane l;
+        l.ua = u_a + (size_t)ct * kN;
+        l.ua2 = u2_a ? u2_a + (size_t)ct * kN : nullptr;
+        l.b = (uint32_t)u_b[ct] + (uint32_t)add_b + (u2_b ? (uint32_t)u2_b[ct] : 0u);
+        l.ra = res_a + (size_t)ct * kn;
+        l.rb = res_b + ct;
+        return l;
+    }
+};
+struct KsRows {                // circuit level: lane ct = g B + k -> wire ks[g].out, instance k
+    const CircKs *ks;
+    const int32_t *u_a, *u_b;
+    int32_t *wa, *wb;
+    int B, nks;
+    __device__ int count() const { return B * nks; }
+    __device__ KsLane lane(int ct) const {
+        const int g = ct / B, k = ct - g * B;
+        const CircKs e = ks[g];
+        const size_t s1 = (size_t)e.r1 * B + k, so = (size_t)e.out * B + k;
+        KsLane l;
+        l.ua = u_a + s1 * kN;
+        l.b = (uint32_t)u_b[s1] + (uint32_t)e.add_b;
+        l.ua2 = nullptr;
+        if (e.r2 >= 0) {
+            const size_t s2 = (size_t)e.r2 * B + k;
+            l.ua2 = u_a + s2 * kN;
+            l.b += (uint32_t)u_b[s2];
+        }
+        l.ra = wa + so * kn;
+        l.rb = wb + so;
+        return l;
+    }
+};
+
+template <class P>
+__global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__restrict__ ksk4, P io) {
     // buf[b][i][j][h][4 cols]: h = 0 is the zero row of lwe-keyswitch-functions.cu:919
     __shared__ __attribute__((aligned(16))) uint4 buf[2][kKs4I * kKsT * 4];   // 2 x 16 KB
     // XCD-aware: workgroups with equal blockIdx % 8 stream the same column blocks
@@ -234,19 +280,18 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(
     if (cb >= kKs4Blocks) return;                 // whole workgroup: no barrier skipped
     const int tid = threadIdx.x;
     const int ct = ctg * kKs4Threads + tid;
-    const bool valid = ct < B;
-    const int ctc = valid ? ct : 0;
+    const bool valid = ct < io.count();
+    const KsLane ln = io.lane(valid ? ct : 0);
     for (int t = tid; t < 2 * kKs4I * kKsT; t += kKs4Threads) buf[t >> 8][(t & 255) * 4] = make_uint4(0, 0, 0, 0);
 
     uint32_t acc[kKs4Cols];
 #pragma unroll
     for (int c = 0; c < kKs4Cols; ++c) acc[c] = 0;
-    if (cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols && valid)
-        acc[kn - cb * kKs4Cols] = (uint32_t)u_b[ct] + (uint32_t)add_b + (u2_b ? (uint32_t)u2_b[ct] : 0u);
+    if (cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols) acc[kn - cb * kKs4Cols] = ln.b;
 
     const uint4 *src = ksk4 + (size_t)cb * kN * kKsT * 3 + tid;
-    const uint4 *pa = reinterpret_cast<const uint4 *>(u_a + (size_t)ctc * kN);
-    const uint4 *pa2 = u2_a ? reinterpret_cast<const uint4 *>(u2_a + (size_t)ctc * kN) : nullptr;
+    const uint4 *pa = reinterpret_cast<const uint4 *>(ln.ua);
+    const uint4 *pa2 = reinterpret_cast<const uint4 *>(ln.ua2);
     // (i, j, h - 1) piece t = tid + 256 l of a chunk goes to buf[.][(t / 3) * 4 + t % 3 + 1]
     int dst[3];
 #pragma unroll
@@ -307,8 +352,8 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(
 #pragma unroll
     for (int c = 0; c < kKs4Cols; ++c) {
         const int col = cb * kKs4Cols + c;
-        if (col < kn) res_a[(size_t)ct * kn + col] = (int32_t)acc[c];
-        else if (col == kn) res_b[ct] = (int32_t)acc[c];
+        if (col < kn) ln.ra[col] = (int32_t)acc[c];
+        else if (col == kn) *ln.rb = (int32_t)acc[c];
     }
 }
 
@@ -324,7 +369,40 @@ __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ k
 
 }  // namespace
 
+hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const CircKs *ks, const int32_t *u_a,
+                                 const int32_t *u_b, int32_t *wa, int32_t *wb, hipStream_t s) {
+    if (B <= 0 || nks <= 0) return hipSuccess;
+    const int groups = (int)(((size_t)B * nks + kKs4Threads - 1) / kKs4Threads);
+    KsRows io{ks, u_a, u_b, wa, wb, B, nks};
+    hipLaunchKernelGGL(k_keyswitch_v4<KsRows>, dim3(128 * groups), dim3(kKs4Threads), 0, s,
+                       reinterpret_cast<const uint4 *>(key.ksk4), io);
+    return hipGetLastError();
+}
+
+// bootstrap-free circuit nodes: W[out] = (0, c) + s W[in]; one thread per (node, instance, word)
+__global__ __launch_bounds__(256) void k_circuit_linear(int B, int nlin, const CircLin *__restrict__ lin,
+                                                        int32_t *__restrict__ wa, int32_t *__restrict__ wb) {
+    const size_t total = (size_t)nlin * B * (kn + 1);
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+        const int w = (int)(t % (kn + 1));
+        const size_t gk = t / (kn + 1);
+        const int g = (int)(gk / B), k = (int)(gk - (size_t)g * B);
+        const CircLin e = lin[g];
+        const size_t so = (size_t)e.out * B + k, si = (size_t)(e.in < 0 ? 0 : e.in) * B + k;
+        if (w < kn) wa[so * kn + w] = e.in < 0 ? 0 : (int32_t)((uint32_t)e.s * (uint32_t)wa[si * kn + w]);
+        else wb[so] = (int32_t)((uint32_t)e.c + (e.in < 0 ? 0u : (uint32_t)e.s * (uint32_t)wb[si]));
+    }
+}
+
 size_t ksk_v4_words() { return (size_t)kKs4Blocks * kN * kKsT * 3 * 4; }
+
+hipError_t launch_circuit_linear(int B, int nlin, const CircLin *lin, int32_t *wa, int32_t *wb, hipStream_t s) {
+    if (B <= 0 || nlin <= 0) return hipSuccess;
+    const size_t total = (size_t)nlin * B * (kn + 1);
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_circuit_linear, dim3(blocks), dim3(256), 0, s, B, nlin, lin, wa, wb);
+    return hipGetLastError();
+}
 
 hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s) {
     hipLaunchKernelGGL(k_ksk_to_v4, dim3(2048), dim3(256), 0, s, d_ksk, reinterpret_cast<uint4 *>(d_ksk4));
@@ -357,8 +435,9 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
                            u2_b, add_b, res_a, res_b);
     } else {
         const int groups = (B + kKs4Threads - 1) / kKs4Threads;
-        hipLaunchKernelGGL(k_keyswitch_v4, dim3(128 * groups), dim3(kKs4Threads), 0, s,
-                           reinterpret_cast<const uint4 *>(key.ksk4), B, u_a, u_b, u2_a, u2_b, add_b, res_a, res_b);
+        KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
+        hipLaunchKernelGGL(k_keyswitch_v4<KsPlain>, dim3(128 * groups), dim3(kKs4Threads), 0, s,
+                           reinterpret_cast<const uint4 *>(key.ksk4), io);
     }
     return hipGetLastError();
 }

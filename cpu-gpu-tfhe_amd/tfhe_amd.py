@@ -381,3 +381,171 @@ class Context:
         _check(lib.tfhe_amd_profile_read(self.h, ctypes.byref(br), ctypes.byref(nb), ctypes.byref(ks),
                                          ctypes.byref(nk)), "profile_read")
         return {"br_ms": br.value, "br_launches": nb.value, "ks_ms": ks.value, "ks_launches": nk.value}
+
+
+# --------------------------------------------------------------------- circuits (§8(f) row 1)
+
+GATES.update({"MAJ": 11, "XOR3": 12, "NOT": 13, "COPY": 14, "CONST": 15})
+_IP = ctypes.POINTER(ctypes.c_int)
+lib.tfhe_amd_circuit_create.argtypes = [ctypes.POINTER(_VP)]
+lib.tfhe_amd_circuit_destroy.argtypes = [_VP]
+lib.tfhe_amd_circuit_inputs.argtypes = [_VP, ctypes.c_int]
+lib.tfhe_amd_circuit_gate.argtypes = [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+lib.tfhe_amd_circuit_lincomb.argtypes = [_VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_int32,
+                                         ctypes.c_int, ctypes.c_int32, ctypes.c_int]
+lib.tfhe_amd_circuit_info.argtypes = [_VP, _IP, _IP, _IP, _IP]
+lib.tfhe_amd_circuit_level_sizes.argtypes = [_VP, _IP, ctypes.c_int]
+lib.tfhe_amd_circuit_node.argtypes = [_VP, ctypes.c_int, _IP, _IP, ctypes.POINTER(ctypes.c_int32),
+                                      ctypes.POINTER(ctypes.c_int32), _IP]
+lib.tfhe_amd_circuit_run_dev.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]
+for _f in ("add", "sub", "add_prefix", "mul"):
+    getattr(lib, "tfhe_amd_circuit_" + _f).argtypes = (
+        [_VP, ctypes.c_int, _IP, _IP] + ([ctypes.c_int] if _f == "add" else []) + [_IP])
+
+
+def _ids(v):
+    return (ctypes.c_int * len(v))(*[int(x) for x in v])
+
+
+class Circuit:
+    """TfheAmdCircuit: gates over SSA wires, evaluated level by level on the GPU for B
+    independent instances (include/tfhe_amd.h, csrc/circuit.cpp)."""
+
+    def __init__(self):
+        h = _VP()
+        _check(lib.tfhe_amd_circuit_create(ctypes.byref(h)), "circuit_create")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.tfhe_amd_circuit_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _w(self, rc, what):
+        if rc < 0:
+            raise TfheAmdError(f"{what} failed with code {rc}")
+        return rc
+
+    def inputs(self, n):
+        first = self._w(lib.tfhe_amd_circuit_inputs(self.h, int(n)), "inputs")
+        return list(range(first, first + n))
+
+    def gate(self, name, a, b=-1, c=-1):
+        g = GATES[name] if isinstance(name, str) else int(name)
+        return self._w(lib.tfhe_amd_circuit_gate(self.h, g, int(a), int(b), int(c)), f"gate {name}")
+
+    def lincomb(self, c0, sa, a, sb=0, b=-1, sc=0, c=-1):
+        return self._w(lib.tfhe_amd_circuit_lincomb(self.h, int(c0), int(sa), int(a), int(sb), int(b), int(sc),
+                                                    int(c)), "lincomb")
+
+    def _vec(self, fn, a, b, n_out, *extra):
+        out = (ctypes.c_int * n_out)()
+        rc = getattr(lib, "tfhe_amd_circuit_" + fn)(self.h, len(a), _ids(a), _ids(b), *extra, out)
+        self._w(rc, fn)
+        return list(out), rc
+
+    def add(self, a, b, carry_in=-1):
+        return self._vec("add", a, b, len(a), int(carry_in))
+
+    def sub(self, a, b):
+        return self._vec("sub", a, b, len(a))
+
+    def add_prefix(self, a, b):
+        return self._vec("add_prefix", a, b, len(a))
+
+    def mul(self, a, b):
+        return self._vec("mul", a, b, 2 * len(a))[0]
+
+    def info(self):
+        v = [ctypes.c_int() for _ in range(4)]
+        _check(lib.tfhe_amd_circuit_info(self.h, *[ctypes.byref(x) for x in v]), "circuit_info")
+        return dict(zip(("wires", "gates", "bootstraps", "depth"), (x.value for x in v)))
+
+    def level_sizes(self):
+        buf = (ctypes.c_int * 4096)()
+        n = self._w(lib.tfhe_amd_circuit_level_sizes(self.h, buf, 4096), "level_sizes")
+        return list(buf[:n])
+
+    def node(self, w):
+        kind, gate = ctypes.c_int(), ctypes.c_int()
+        c0 = ctypes.c_int32()
+        s = (ctypes.c_int32 * 3)()
+        ins = (ctypes.c_int * 3)()
+        _check(lib.tfhe_amd_circuit_node(self.h, int(w), ctypes.byref(kind), ctypes.byref(gate), ctypes.byref(c0),
+                                         s, ins), "circuit_node")
+        return kind.value, gate.value, c0.value, list(s), list(ins)
+
+    def eval_plain(self, bits):
+        """Plaintext evaluation of the circuit as built (host; test oracle for the builders):
+        wire encodings are +-2^29 and every bootstrapped row is the sign of its torus sum,
+        so the threshold gates are checked in the same arithmetic the GPU rows use.
+        bits: {input wire: 0/1 array}; returns {wire: 0/1 array} for all wires."""
+        e8 = 1 << 29
+        n_w = self.info()["wires"]
+        val = {}
+
+        def enc(w):
+            return val[w]
+        spec = {0: (e8, -1, -1), 1: (e8, 1, 1), 2: (-e8, 1, 1), 3: (1 << 30, 2, 2), 4: (-(1 << 30), -2, -2),
+                5: (-e8, -1, -1), 6: (-e8, -1, 1), 7: (-e8, 1, -1), 8: (e8, -1, 1), 9: (e8, 1, -1)}
+
+        def sign(x):   # torus phase > 0 (int32)
+            x = (np.asarray(x, dtype=np.int64) + 2**31) % 2**32 - 2**31
+            return np.where(x > 0, e8, -e8).astype(np.int64)
+        for w in range(n_w):
+            kind, gate, c0, s, ins = self.node(w)
+            if kind == 0:
+                val[w] = np.where(np.asarray(bits[w]) != 0, e8, -e8).astype(np.int64)
+            elif kind == 2:
+                if gate == GATES["CONST"]:
+                    val[w] = np.int64(c0)
+                else:
+                    val[w] = (-1 if gate == GATES["NOT"] else 1) * enc(ins[0])
+            elif gate == GATES["MUX"]:
+                u1 = sign(-e8 + enc(ins[0]) + enc(ins[1]))
+                u2 = sign(-e8 - enc(ins[0]) + enc(ins[2]))
+                val[w] = sign(e8 + u1 + u2)
+            else:
+                if gate in spec:
+                    c, sa, sb = spec[gate]
+                    x = c + sa * enc(ins[0]) + sb * enc(ins[1])
+                else:
+                    x = c0 + sum(s[t] * enc(ins[t]) for t in range(3) if ins[t] >= 0)
+                val[w] = sign(x)
+        return {w: (np.asarray(v) > 0).astype(np.int64) for w, v in val.items()}
+
+    def run(self, ctx, B, inputs, outputs, keyset, rng, stream=None):
+        """Encrypt `inputs` ({wire: bit array [B]}), run on the GPU, decrypt `outputs`
+        (list of wires) -> {wire: bit array}.  Convenience for tests and the bench."""
+        import torch
+        n_w = self.info()["wires"]
+        wa = torch.zeros((n_w, B, n_lwe), dtype=torch.int32, device="cuda")
+        wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+        for w, bits in inputs.items():
+            a, b = keyset.encrypt(np.asarray(bits), rng)
+            wa[w] = torch.from_numpy(a).cuda()
+            wb[w] = torch.from_numpy(b).cuda()
+        self.run_dev(ctx, B, wa, wb, stream)
+        torch.cuda.synchronize()
+        ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+        return {w: keyset.decrypt(ha[w], hb[w]) for w in outputs}
+
+    def run_dev(self, ctx, B, wa, wb, stream=None):
+        _check(lib.tfhe_amd_circuit_run_dev(ctx.h, self.h, int(B), wa.data_ptr(), wb.data_ptr(), stream),
+               "circuit_run_dev")
+
+
+def bits_of(x, nbits):
+    """little-endian bit planes of an integer array: [nbits][B]"""
+    x = np.asarray(x, dtype=np.int64)
+    return [((x >> i) & 1) for i in range(nbits)]
+
+
+def int_of(planes):
+    return sum(np.asarray(p, dtype=np.int64) << i for i, p in enumerate(planes))

@@ -38,7 +38,13 @@ enum {
 enum {
     TFHE_GATE_NAND = 0, TFHE_GATE_OR = 1, TFHE_GATE_AND = 2, TFHE_GATE_XOR = 3,
     TFHE_GATE_XNOR = 4, TFHE_GATE_NOR = 5, TFHE_GATE_ANDNY = 6, TFHE_GATE_ANDYN = 7,
-    TFHE_GATE_ORNY = 8, TFHE_GATE_ORYN = 9, TFHE_GATE_MUX = 10
+    TFHE_GATE_ORNY = 8, TFHE_GATE_ORYN = 9, TFHE_GATE_MUX = 10,
+    /* circuit-only gates (below): */
+    TFHE_GATE_MAJ = 11,    /* majority(a, b, c), one bootstrap */
+    TFHE_GATE_XOR3 = 12,   /* a ^ b ^ c, one bootstrap */
+    TFHE_GATE_NOT = 13,    /* bootsNOT (boot-gates.cu:242): linear, no bootstrap */
+    TFHE_GATE_COPY = 14,   /* bootsCOPY: linear */
+    TFHE_GATE_CONST = 15   /* bootsCONSTANT: `a` is the bit value, no inputs */
 };
 
 typedef struct TfheAmdContext TfheAmdContext;
@@ -133,6 +139,46 @@ int tfhe_amd_select_kernel(int br_version);
 
 /* build tag, e.g. "tfhe_amd gfx950 ntt2x30 br-v1" */
 const char *tfhe_amd_version(void);
+
+/* ---------------------------------------------------------------- circuits (§8(f) row 1)
+ * A circuit is a DAG of gates over SSA wires (ids 0, 1, ... in creation order; every wire
+ * is written once).  tfhe_amd_circuit_run_dev evaluates B independent instances: wires are
+ * device arrays a [n_wires][B][500], b [n_wires][B] (wire w of instance k at w*B + k), the
+ * input wires filled by the caller.  The compiler levels the DAG by bootstrap depth; each
+ * level is ONE blind-rotation launch over all of its gates x B instances and ONE key-switch
+ * launch (the reference's compound ANDXOR / XORXOR gates, boot-gates.cu:3027-3098, are the
+ * two-gate case).  NOT / COPY / CONST cost no bootstrap: they are folded into the gates that
+ * read them (and also written to their own wires).
+ * Builders return the new wire id (>= 0) or a negative TFHE_AMD_E* code. */
+typedef struct TfheAmdCircuit TfheAmdCircuit;
+int tfhe_amd_circuit_create(TfheAmdCircuit **out);
+int tfhe_amd_circuit_destroy(TfheAmdCircuit *c);
+/* `count` fresh input wires; returns the first id */
+int tfhe_amd_circuit_inputs(TfheAmdCircuit *c, int count);
+/* one gate (TFHE_GATE_*); unused inputs ignored (MUX: a ? b : cc; CONST: a = bit value) */
+int tfhe_amd_circuit_gate(TfheAmdCircuit *c, int gate, int a, int b, int cc);
+/* a bootstrapped linear combination: sign((0, c0) + sa*a + sb*b + sc*cc) -> {-1/8, +1/8}
+ * (b, cc may be -1); the building block of threshold gates */
+int tfhe_amd_circuit_lincomb(TfheAmdCircuit *c, int32_t c0, int32_t sa, int a, int32_t sb, int b, int32_t sc,
+                             int cc);
+/* node w as built: kind 0 input / 1 bootstrapped / 2 linear, gate code (-1 = lincomb),
+ * constant, coefficients[3], inputs[3] (for host-side plaintext evaluation in tests) */
+int tfhe_amd_circuit_node(const TfheAmdCircuit *c, int w, int *kind, int *gate, int32_t *c0, int32_t *s, int *in);
+/* compile (if needed) and report size: wires, gates, bootstraps per instance, depth */
+int tfhe_amd_circuit_info(TfheAmdCircuit *c, int *n_wires, int *n_gates, int *n_bootstraps, int *depth);
+/* rows (bootstraps) per level, level 0 first (level 0 is bootstrap-free); returns #levels */
+int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_level, int cap);
+int tfhe_amd_circuit_run_dev(TfheAmdContext *ctx, TfheAmdCircuit *c, int B, int32_t *wires_a, int32_t *wires_b,
+                             void *stream);
+/* integer builders over little-endian bit vectors of wire ids (Cipher.cpp's layout):
+ * ripple-carry add (XOR3 / MAJ full adders, depth nbits; carry_in may be -1) -> carry wire;
+ * subtract a - b -> carry wire; parallel-prefix add (depth 2 + log2 nbits) -> carry wire;
+ * unsigned multiply nbits x nbits -> 2 nbits (AND partial products, carry-save tree,
+ * prefix adder) */
+int tfhe_amd_circuit_add(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int carry_in, int *sum);
+int tfhe_amd_circuit_sub(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *diff);
+int tfhe_amd_circuit_add_prefix(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *sum);
+int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *prod);
 
 #ifdef __cplusplus
 }
