@@ -419,18 +419,17 @@ extern "C" int tfhe_amd_circuit_add_prefix(TfheAmdCircuit *c, int nbits, const i
     return G_[nbits - 1];
 }
 
-// unsigned n x n -> 2n multiplier: n^2 partial products (one level of ANDs, the reference's
-// bootsAND over iBits^2, main.cu:1506-1528), a Dadda carry-save tree (one level per stage:
-// full adders = XOR3 + MAJ, half adders = XOR + AND, target heights 2, 3, 4, 6, 9, 13, ...),
-// then a parallel-prefix adder for the last two rows.  Depth 1 + stages + 2 + log2(2n).
-extern "C" int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *prod) {
-    if (!c || nbits <= 0 || !a || !b || !prod) return TFHE_AMD_E_ARG;
-    const int W = 2 * nbits;
-    std::vector<std::vector<int>> col(W);
-    for (int i = 0; i < nbits; ++i)
-        for (int j = 0; j < nbits; ++j) col[i + j].push_back(G(c, TFHE_GATE_AND, a[j], b[i]));
+namespace {
+
+// Dadda reduction of bit columns (col[k] = wires of weight 2^k) to two rows, one level per
+// stage (full adders = XOR3 + MAJ, half adders = XOR + AND; target heights 2, 3, 4, 6, 9,
+// 13, ...), then a parallel-prefix adder: out[0 .. W) = the column sum mod 2^W.
+void reduce_columns(TfheAmdCircuit *c, std::vector<std::vector<int>> col, int *out) {
+    const int W = (int)col.size();
+    size_t h0 = 0;
+    for (auto &v : col) h0 = std::max(h0, v.size());
     std::vector<int> targets{2};
-    while (targets.back() < nbits) targets.push_back(targets.back() * 3 / 2);
+    while (targets.back() < (int)h0) targets.push_back(targets.back() * 3 / 2);
     for (int st = (int)targets.size() - 1; st >= 0; --st) {
         const int d = targets[st];
         size_t hmax = 0;
@@ -469,6 +468,35 @@ extern "C" int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, 
         x[k] = col[k].size() > 0 ? col[k][0] : zero;
         y[k] = col[k].size() > 1 ? col[k][1] : zero;
     }
-    tfhe_amd_circuit_add_prefix(c, W, x.data(), y.data(), prod);
+    tfhe_amd_circuit_add_prefix(c, W, x.data(), y.data(), out);
+}
+
+}  // namespace
+
+// unsigned n x n -> 2n multiplier: n^2 partial products (one level of ANDs, the reference's
+// bootsAND over iBits^2, main.cu:1506-1528), a Dadda carry-save tree and a parallel-prefix
+// adder for the last two rows.  Depth 1 + stages + 2 + log2(2n).
+extern "C" int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *prod) {
+    if (!c || nbits <= 0 || !a || !b || !prod) return TFHE_AMD_E_ARG;
+    std::vector<std::vector<int>> col(2 * nbits);
+    for (int i = 0; i < nbits; ++i)
+        for (int j = 0; j < nbits; ++j) col[i + j].push_back(G(c, TFHE_GATE_AND, a[j], b[i]));
+    reduce_columns(c, std::move(col), prod);
+    return TFHE_AMD_OK;
+}
+
+// dot product of nterms pairs of unsigned nbits integers: sum_t a_t * b_t into out_bits bits
+// (mod 2^out_bits; 2 nbits + ceil(log2 nterms) bits are exact).  All nterms * nbits^2
+// partial products go into ONE Dadda tree (no per-term multiplier + adder tree as in the
+// reference's BOOTS_matrixMultiplication, main.cu:2342-2462): depth 1 + stages + prefix.
+extern "C" int tfhe_amd_circuit_dot(TfheAmdCircuit *c, int nterms, int nbits, const int *a, const int *b,
+                                    int out_bits, int *out) {
+    if (!c || nterms <= 0 || nbits <= 0 || out_bits <= 0 || !a || !b || !out) return TFHE_AMD_E_ARG;
+    std::vector<std::vector<int>> col(out_bits);
+    for (int t = 0; t < nterms; ++t)
+        for (int i = 0; i < nbits; ++i)
+            for (int j = 0; j < nbits; ++j)
+                if (i + j < out_bits) col[i + j].push_back(G(c, TFHE_GATE_AND, a[t * nbits + j], b[t * nbits + i]));
+    reduce_columns(c, std::move(col), out);
     return TFHE_AMD_OK;
 }

@@ -398,6 +398,7 @@ lib.tfhe_amd_circuit_level_sizes.argtypes = [_VP, _IP, ctypes.c_int]
 lib.tfhe_amd_circuit_node.argtypes = [_VP, ctypes.c_int, _IP, _IP, ctypes.POINTER(ctypes.c_int32),
                                       ctypes.POINTER(ctypes.c_int32), _IP]
 lib.tfhe_amd_circuit_run_dev.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]
+lib.tfhe_amd_circuit_dot.argtypes = [_VP, ctypes.c_int, ctypes.c_int, _IP, _IP, ctypes.c_int, _IP]
 for _f in ("add", "sub", "add_prefix", "mul"):
     getattr(lib, "tfhe_amd_circuit_" + _f).argtypes = (
         [_VP, ctypes.c_int, _IP, _IP] + ([ctypes.c_int] if _f == "add" else []) + [_IP])
@@ -461,6 +462,15 @@ class Circuit:
 
     def mul(self, a, b):
         return self._vec("mul", a, b, 2 * len(a))[0]
+
+    def dot(self, a_terms, b_terms, out_bits):
+        """sum_t a_t * b_t: a_terms / b_terms are lists of bit-vectors (little-endian wires)"""
+        nt, nb = len(a_terms), len(a_terms[0])
+        fa = [w for v in a_terms for w in v]
+        fb = [w for v in b_terms for w in v]
+        out = (ctypes.c_int * out_bits)()
+        self._w(lib.tfhe_amd_circuit_dot(self.h, nt, nb, _ids(fa), _ids(fb), int(out_bits), out), "dot")
+        return list(out)
 
     def info(self):
         v = [ctypes.c_int() for _ in range(4)]

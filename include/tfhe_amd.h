@@ -179,6 +179,10 @@ int tfhe_amd_circuit_add(TfheAmdCircuit *c, int nbits, const int *a, const int *
 int tfhe_amd_circuit_sub(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *diff);
 int tfhe_amd_circuit_add_prefix(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *sum);
 int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *prod);
+/* sum_t a_t * b_t over nterms pairs of nbits-bit operands (a, b: nterms * nbits wires, term
+ * major) into out_bits bits, mod 2^out_bits: one Dadda tree over all partial products */
+int tfhe_amd_circuit_dot(TfheAmdCircuit *c, int nterms, int nbits, const int *a, const int *b, int out_bits,
+                         int *out);
 
 #ifdef __cplusplus
 }
