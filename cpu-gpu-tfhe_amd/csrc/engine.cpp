@@ -68,17 +68,31 @@ void build_ntt_tables(NttTables *t) {
     t->crt_hp = shoup(t->crt_h, kQ[1]);
 }
 
-static std::atomic<int> g_br_version{0};
+static std::atomic<int> g_br_version{-1};
 
 int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
-    if (v == 0) {
+    if (v < 0) {
         const char *e = getenv("TFHE_AMD_BR");
-        v = e ? atoi(e) : 4;
-        if (v < 1 || v > 4) v = 4;
+        v = e ? atoi(e) : 0;
+        if (v < 0 || v > 5) v = 0;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
+}
+
+// auto mode: the latency kernel (8 waves per ciphertext, one per CU) while a launch has few
+// ciphertexts; the throughput kernel (2 waves, 4 per CU) once it fills the chip
+static long v5_threshold() {
+    static const long t = [] {
+        const char *e = getenv("TFHE_AMD_V5_MAX");
+        return e ? atol(e) : 512L;
+    }();
+    return t;
+}
+bool use_v5(long count) {
+    const int v = br_version();
+    return v == 5 || (v == 0 && count <= v5_threshold());
 }
 
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
@@ -87,7 +101,11 @@ static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput 
     case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
     case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
     case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
-    default: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
+    case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
+    case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
+    default:
+        return use_v5((long)B * halves) ? launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s)
+                                        : launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     }
 }
 
@@ -443,7 +461,7 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
            : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
            : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
-                    : launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s));
+                    : launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s));   // v5 shares v4's math
     return TFHE_AMD_OK;
 }
 
@@ -561,19 +579,21 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version < 1 || br_version > 4) return TFHE_AMD_E_ARG;
+    if (br_version < 0 || br_version > 5) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }
 
 extern "C" const char *tfhe_amd_version(void) {
     // one immutable string per (blind-rotation, key-switch) generation pair
-    static char names[5][5][48];
+    static char names[6][5][48];
     static std::once_flag once;
     std::call_once(once, [] {
-        for (int b = 1; b <= 4; b++)
-            for (int k = 1; k <= 4; k++)
-                snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
+        for (int b = 0; b <= 5; b++)
+            for (int k = 1; k <= 4; k++) {
+                if (b == 0) snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v4v5 ks-v%d", k);
+                else snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
+            }
     });
     return names[br_version()][ks_version()];
 }

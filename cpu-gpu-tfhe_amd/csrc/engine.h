@@ -76,7 +76,14 @@ hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, 
 // circuit level (v4 kernel): B instances x nrows rows, wires [W][B] ciphertexts, u slots r B + k
 hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
-// which blind-rotation kernel runs: 1..4 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
+// v5 (latency: 8 waves per ciphertext), blind_rotate_v5.hip; same results as v4
+hipError_t launch_blind_rotate_v5(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v5_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+// v4 vs v5 for `count` blind rotations in one launch (br_version 0 = auto)
+bool use_v5(long count);
+// which blind-rotation kernel runs: 0 = auto (v5 for small launches, v4 otherwise), 1..5 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 
 // which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)

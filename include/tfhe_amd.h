@@ -130,10 +130,11 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 /* TLWE secret key (int32 [1024]; k = 1), = the extracted LWE key of woKS outputs */
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
-/* Select the blind-rotation kernel generation (1 = LDS radix-2 reference kernel,
+/* Select the blind-rotation kernel generation: 0 = auto (the default: v5 for launches of at
+ * most TFHE_AMD_V5_MAX = 512 blind rotations, v4 above), 1 = LDS radix-2 reference kernel,
  * 2 = register-resident NTT with 2 waves per ciphertext, 3 = 4 waves per ciphertext,
- * 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT and a periodic accumulator, the
- * default; env TFHE_AMD_BR=<n> does the same at startup).
+ * 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT and a periodic accumulator (throughput),
+ * 5 = 8 waves per ciphertext (latency); env TFHE_AMD_BR=<n> does the same at startup.
  * For A/B measurements and parity cross-checks; results are identical by contract. */
 int tfhe_amd_select_kernel(int br_version);
 

@@ -134,15 +134,16 @@ def test_kernel_generations_agree(ctx, keyset, rng):
     default = T.version()
     outs = {}
     try:
-        for v in (1, 2, 3, 4):
+        for v in (1, 2, 3, 4, 5):
             T.select_kernel(v)
             d_acc = torch.from_numpy(acc0.copy()).cuda()
             ctx.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), iters)
             ctx.sync()
             outs[v] = (ctx.gate_host("XOR", a_a, a_b, b_a, b_b), d_acc.cpu().numpy())
     finally:
-        T.select_kernel(int(default.split("br-v")[1][0]))
-    for v in (1, 2, 3):
+        tag = default.split("br-v")[1].split(" ")[0]
+        T.select_kernel(0 if tag == "4v5" else int(tag))
+    for v in (1, 2, 3, 5):
         (ra, rb), acc = outs[v]
         (ra4, rb4), acc4 = outs[4]
         assert np.array_equal(ra, ra4) and np.array_equal(rb, rb4), v
