@@ -98,7 +98,8 @@ __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, in
             D[2 * c][r] = ((t >> 22) & 1023u) + (q - 512u);
             D[2 * c + 1][r] = ((t >> 12) & 1023u) + (q - 512u);
         }
-    ntt_fwd<4>(D, sc, g.tu_f + 16 * s, g.ts_f + s * 27 * 64 + L, L, q);
+    const uint2 *tsf = g.ts_f + s * 27 * 64 + L, *tsi = g.ts_i + s * 27 * 64 + L, *tpb = g.tpost + s * 16 * 64 + L;
+    ntt_fwd<4>(D, sc, g.tu_f + 16 * s, tsf, L, q);
     // pointwise MAC with BK_i (layout C: reg r = 4 v + e <-> slot 16 L + r), REDC lazy
     const uint4 *bk4 = reinterpret_cast<const uint4 *>(g.bk + ((size_t)(i * 2 + s) * 8) * kN) + L;
     const uint32_t qinv = s ? g.qinv_neg1 : g.qinv_neg0;
@@ -124,9 +125,9 @@ __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, in
             }
         }
     }
-    ntt_inv_ct<2>(O, sc, g.tu_i + 16 * s, g.ts_i + s * 27 * 64 + L, L, q);   // < 23.75 q, layout A
+    ntt_inv_ct<2>(O, sc, g.tu_i + 16 * s, tsi, L, q);   // < 31.75 q, layout A
     {   // post-twist psi^-n (n = L + 64 r) -> [0, 2q)
-        const uint2 *tp = g.tpost + s * 16 * 64 + L;
+        const uint2 *tp = tpb;
         const uint32_t negq = 0u - q;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
