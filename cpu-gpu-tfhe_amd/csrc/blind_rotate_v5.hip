@@ -22,6 +22,22 @@ namespace tfhe_amd {
 namespace {
 
 constexpr int kV5Threads = 512;
+
+#ifdef TFHE_AMD_V5_STAMPS
+// timing diagnostics: cumulative shader-clock cycles per phase for waves 0 (MAC) and 2 (idle)
+// of workgroup 0; read with tfhe_amd_debug_v5_stamps
+__device__ unsigned long long g_v5_stamps[2][12];
+#define V5_STAMP(k)                                                                         \
+    do {                                                                                     \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && (tid & 63) == 0 && (w == 0 || w == 2)) { \
+            const unsigned long long now = __builtin_amdgcn_s_memtime();                     \
+            g_v5_stamps[w >> 1][k] += now - t_prev;                                          \
+            t_prev = now;                                                                    \
+        }                                                                                    \
+    } while (0)
+#else
+#define V5_STAMP(k) do {} while (0)
+#endif
 constexpr int kExt5 = 3 * kN;
 
 struct V5Shared {
@@ -62,6 +78,15 @@ __device__ __forceinline__ void load_bk(const V5Args &g, int i, int s, int c, in
     for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int v = 0; v < 4; ++v) b[p][v] = bk4[(c * 4 + p) * 256 + v * 64];
+}
+
+// Workgroup barrier for LDS traffic only.  __syncthreads() is a workgroup-scope release /
+// acquire fence around s_barrier, which also waits for every outstanding GLOBAL load
+// (vmcnt(0)) — i.e. for the next step's BK_i prefetch, defeating it.  The step loop has no
+// global stores, so an LDS-only wait + s_barrier is sufficient; the asm "memory" clobber
+// keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int S>
@@ -128,6 +153,9 @@ __device__ __forceinline__ void br_v5_body(V5Shared &sh, const V5Args &g, const 
     uint32_t *sc = sh.scratch[w];
     uint4 bk[4][4];
     int inext = 0;
+#ifdef TFHE_AMD_V5_STAMPS
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
     while (inext < kn && sh.bara[inext] == 0) ++inext;
     if (mac && inext < kn) load_bk(g, inext, s, c_out, L, bk);
     for (int i = inext; i < kn;) {
@@ -146,9 +174,12 @@ __device__ __forceinline__ void br_v5_body(V5Shared &sh, const V5Args &g, const 
             }
         }
         const uint2 *tsf = &sh.tsf[s][0][L], *tsi = &sh.tsi[s][0][L], *tp = &sh.tpost[s][0][L];
+        V5_STAMP(0);
         ntt_fwd<1>(D, sc, g.tu_f + 16 * s, tsf, L, q);
         store_C(sc, D[0], L);                                   // this wave's digit poly, NTT domain
-        __syncthreads();                                        // B1: all digits in LDS
+        V5_STAMP(1);
+        lds_barrier();                                          // B1: all digits in LDS
+        V5_STAMP(2);
         uint32_t O[1][16];
         if (mac) {
             // 2. MAC for output c_out over 16 slots per lane (slot 16 L + r), REDC lazy
@@ -172,10 +203,13 @@ __device__ __forceinline__ void br_v5_body(V5Shared &sh, const V5Args &g, const 
             }
             if (j < kn) load_bk(g, j, s, c_out, L, bk);         // next step's key, in flight
         }
-        __syncthreads();                                        // B1b: digit polys consumed
+        V5_STAMP(3);
+        lds_barrier();                                          // B1b: digit polys consumed
+        V5_STAMP(4);
         if (mac) {
             // 3. inverse NTT + post-twist (layout A: coefficient L + 64 r)
             ntt_inv_ct<1>(O, sc, g.tu_i + 16 * s, tsi, L, q);
+            V5_STAMP(5);
             const uint32_t negq = 0u - q;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -186,13 +220,17 @@ __device__ __forceinline__ void br_v5_body(V5Shared &sh, const V5Args &g, const 
             if (s == 0) crt5_give<0>(sc, O[0], L);
             else crt5_give<1>(sc, O[0], L);
         }
-        __syncthreads();                                        // B2 (uniform control flow)
+        V5_STAMP(6);
+        lds_barrier();                                          // B2 (uniform control flow)
+        V5_STAMP(7);
         if (mac) {
             // 4b. CRT take + accumulate into E (both primes' residues of the kept half)
             if (s == 0) crt5_take<0>(sh, sh.scratch[w ^ 4], O[0], c_out, L, g);
             else crt5_take<1>(sh, sh.scratch[w ^ 4], O[0], c_out, L, g);
         }
-        __syncthreads();                                        // B3: E updated
+        V5_STAMP(8);
+        lds_barrier();                                          // B3: E updated
+        V5_STAMP(9);
         i = j;
     }
     for (int j = tid; j < kN; j += kV5Threads) ua[j] = (int32_t)sh.E[0][(k2N - j) & (k2N - 1)];
@@ -254,6 +292,21 @@ static V5Args v5_args(const DeviceKey &key) {
     g.crt_hp = key.crt_hp;
     return g;
 }
+
+#ifdef TFHE_AMD_V5_STAMPS
+}  // namespace tfhe_amd
+extern "C" int tfhe_amd_debug_v5_stamps(unsigned long long *out, int reset) {
+    unsigned long long h[24];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(tfhe_amd::g_v5_stamps), sizeof h) != hipSuccess) return -2;
+    for (int i = 0; i < 24; i++) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[24] = {0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(tfhe_amd::g_v5_stamps), z, sizeof z);
+    }
+    return 0;
+}
+namespace tfhe_amd {
+#endif
 
 hipError_t launch_blind_rotate_v5(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                   int32_t *u_a, int32_t *u_b, hipStream_t s) {

@@ -113,11 +113,25 @@ __device__ __forceinline__ void load_C(const uint32_t *sc, uint32_t (&x)[16], in
     }
 }
 
+// stream twiddle `slot` for this lane: from the up-front copy (NP == 1) or loaded now
+template <int NP>
+__device__ __forceinline__ uint2 tw_slot(const uint2 (&tall)[NP == 1 ? 27 : 1], const uint2 *__restrict__ ts, int slot) {
+    if constexpr (NP == 1) return tall[slot];
+    else return ts[TW_SLOT(slot * 64)];
+}
+
 // ---- forward NTT of NP polys (layout A in, layout C out), values < 2q in, < 22q out
+// (NP == 1, the latency kernel: all 27 stream twiddles are read at entry, before the layout-A
+// stages and the transposes, so no stage group waits for its twiddle load)
 template <int NP>
 __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
                                         const uint2 *__restrict__ ts, int L, uint32_t q) {
     const uint32_t q2 = 2 * q;
+    uint2 tall[NP == 1 ? 27 : 1];
+    if constexpr (NP == 1) {
+#pragma unroll
+        for (int g = 0; g < 27; ++g) tall[g] = ts[TW_SLOT(g * 64)];
+    }
 #pragma unroll
     for (int K = 9; K >= 6; --K) {                     // layout A, uniform twiddles
         const int d = 1 << (K - 6);
@@ -142,7 +156,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
         const int d = 1 << (K - 2), cnt = 1 << (5 - K);
         uint2 tw[8];
 #pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[TW_SLOT((slot + g) * 64)];
+        for (int g = 0; g < cnt; ++g) tw[g] = tw_slot<NP>(tall, ts, slot + g);
         slot += cnt;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -164,7 +178,7 @@ __device__ __forceinline__ void ntt_fwd(uint32_t (&x)[NP][16], uint32_t *sc, con
         const int d = 1 << K, cnt = 1 << (3 - K);
         uint2 tw[8];
 #pragma unroll
-        for (int g = 0; g < cnt; ++g) tw[g] = ts[TW_SLOT((slot + g) * 64)];
+        for (int g = 0; g < cnt; ++g) tw[g] = tw_slot<NP>(tall, ts, slot + g);
         slot += cnt;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -251,6 +265,11 @@ template <int NP>
 __device__ __forceinline__ void ntt_inv_ct(uint32_t (&x)[NP][16], uint32_t *sc, const uint2 *__restrict__ tu,
                                            const uint2 *__restrict__ ts, int L, uint32_t q) {
     const uint32_t q2 = 2 * q;
+    uint2 tall[NP == 1 ? 27 : 1];                      // NP == 1: all stream twiddles up front
+    if constexpr (NP == 1) {
+#pragma unroll
+        for (int g = 0; g < 27; ++g) tall[g] = ts[TW_SLOT(g * 64)];
+    }
 #pragma unroll
     for (int S = 0; S <= 3; ++S) {                     // layout C, uniform twiddles
         const int d = 1 << S;
@@ -288,7 +307,7 @@ __device__ __forceinline__ void ntt_inv_ct(uint32_t (&x)[NP][16], uint32_t *sc, 
         const int d = 1 << (S - 2);
         uint2 tw[8];
 #pragma unroll
-        for (int g = 0; g < d; ++g) tw[g] = ts[TW_SLOT((slot + g) * 64)];
+        for (int g = 0; g < d; ++g) tw[g] = tw_slot<NP>(tall, ts, slot + g);
         slot += d;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -310,7 +329,7 @@ __device__ __forceinline__ void ntt_inv_ct(uint32_t (&x)[NP][16], uint32_t *sc, 
         const int d = 1 << (S - 6);
         uint2 tw[8];
 #pragma unroll
-        for (int g = 0; g < d; ++g) tw[g] = ts[TW_SLOT((slot + g) * 64)];
+        for (int g = 0; g < d; ++g) tw[g] = tw_slot<NP>(tall, ts, slot + g);
         slot += d;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
