@@ -93,9 +93,18 @@ def main():
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") on the 8-GPU node.  TFHE_AMD_DIST_BACKEND=gloo rehearses the N>1 path with
+    # several ranks sharing the GPUs that exist (ranks map to device LOCAL_RANK mod count).
+    backend = os.environ.get("TFHE_AMD_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     K = T.SecretKeyset()                   # real keys (seed 314,1592,657), ~1 s on the host
     rng = np.random.default_rng(1000 + rank)
@@ -126,7 +135,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device="cuda")
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=red_dev)
 
     # correctness guard on the last step's output (truth table; cheap)
     dec = K.decrypt(r_a.cpu().numpy(), r_b.cpu().numpy())
