@@ -9,9 +9,15 @@ rank processes its own shard of independent ciphertexts; no collective on the da
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
 Rank 0 prints ONE JSON line.  Extra objects:
-  roofline     : the blind-rotation kernel's streamed bootstrapping-key bytes (SURVEY.md §8(d):
-                 32 768 000 B per bootstrap) / its average launch time (HIP events on the
-                 stream it runs on) vs the 8 TB/s HBM peak; traffic from profiles/ PMC data.
+  roofline     : the dominant kernel = the blind rotation (k_blind_rotate_v6, fp64 FFT external
+                 product).  It is bound by fp64 VALU issue, not HBM (the 32.8 MB key stream per
+                 bootstrap is shared by the whole batch and served from L2/MALL: PMC traffic is
+                 ~2.5 % of it), so `achieved` = its algorithmic fp64 FLOPs (193 536 per CMux
+                 step x 500 steps per bootstrap x B; FMA = 2) / its average launch time (HIP
+                 events on the stream it runs on) vs the 78.6 TFLOP/s fp64 vector peak; traffic
+                 = HBM bytes per launch from the profiles/ PMC data.  The key-stream rate is
+                 reported beside it (`key_stream_GBps`).  With an exact-NTT kernel pinned
+                 (TFHE_AMD_BR=1..5) the line falls back to the key-stream / HBM framing.
   cpu_baseline : the CPU restatement (oracle/, same algorithm, exact NTT, OpenMP) timed on
                  this host's cores on a bounded sample of the same workload (rank 0, N=1).
 """
@@ -29,6 +35,12 @@ sys.path.insert(0, os.path.join(REPO, "cpu-gpu-tfhe_amd"))
 BK_BYTES_PER_BOOTSTRAP = 500 * 4 * 2 * 1024 * 8        # NTT-domain TGSW key stream, 32 768 000 B
 KS_BYTES_PER_KEYSWITCH = 1024 * 8 * 501 * 4            # KSK rows, 16 416 768 B
 HBM_PEAK_GBPS = 8000.0
+# v6 fp64 work per CMux step (blind_rotate_v6.hip): 4 forward transforms x 2304
+# butterflies x 12 + 2 inverse x 2304 x 10 + MAC 2 x 4 x 512 x 7 + partial sums 2048 +
+# mod-2^32 rounding 2048 x 3
+FLOPS_PER_CMUX = 4 * 2304 * 12 + 2 * 2304 * 10 + 2 * 4 * 512 * 7 + 2048 + 2048 * 3   # 193 536
+FLOPS_PER_BOOTSTRAP = 500 * FLOPS_PER_CMUX
+FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP), AMD spec
 
 
 def parse():
@@ -150,7 +162,19 @@ def main():
     ctx.profile_enable(False)
     br_ms = prof["br_ms"] / max(1, prof["br_launches"])
     ks_ms = prof["ks_ms"] / max(1, prof["ks_launches"])
-    achieved = B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9
+    key_gbps = B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9
+    fft = "fft64" in T.version()
+    if fft:
+        achieved = B * FLOPS_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(T.version(), B),
+                "kernel": "k_blind_rotate_v6", "dtype": "f64", "flops_per_launch": B * FLOPS_PER_BOOTSTRAP}
+    else:
+        roof = {"bound": "hbm", "achieved": key_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": key_gbps / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
+                "kernel": "k_blind_rotate"}
+    roof.update({"kernel_ms": br_ms, "keyswitch_ms": ks_ms, "key_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP,
+                 "key_stream_GBps": key_gbps})
 
     value = shard.weak_scaling_value(B, world, args.steps, elapsed)
     line = {
@@ -164,15 +188,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32 (Torus32; exact 2x27-bit CRT NTT)",
+        "dtype": ("f64 (FFT external product; Torus32 in/out, rounded products exact)" if fft
+                  else "int32 (Torus32; exact 2x27-bit CRT NTT)"),
         "data": "synthetic: random bits encrypted under keys generated from seed {314,1592,657}",
         "config": {"workload": f"batch of {B} independent boots{args.gate} per GPU (BASELINE configs[1])",
                    "batch_per_gpu": B, "gate": args.gate, "params": "n=500 N=1024 k=1 l=2 Bgbit=10 ks_t=8 ks_basebit=2",
                    "parallelism": f"shard{world} (independent ciphertexts, no collective)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
-                     "kernel": "k_blind_rotate", "kernel_ms": br_ms, "keyswitch_ms": ks_ms,
-                     "algorithmic_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP},
+        "roofline": roof,
         "truth_table_ok": truth_ok,
         "engine": T.version(),
     }

@@ -1,0 +1,546 @@
+// blind_rotate_v6.hip — blind rotation with an fp64 negacyclic FFT external product.
+//
+// The reference computes tGswFFTExternMulToTLwe with a double-precision FFT
+// (tgsw-fft-operations.cu:124-264: IntPolynomial_ifft of the decomposition, the
+// LagrangeHalfCPolynomial MAC with the FFT-domain key, TorusPolynomial_fft back).  v1..v5 use an
+// exact 2-prime NTT instead; on CDNA4 that costs ~22 VALU issue cycles per radix-2 butterfly
+// per prime, where the fp64 butterfly below costs 6 full-rate v_fma_f64 (MI355X: fp64 vector
+// FMA at the fp32 rate), so v6 returns to the reference's arithmetic, MI355X-shaped:
+//
+//  * one ciphertext = 2 waves (128 threads, 4 workgroups per CU); wave w owns accumulator
+//    polynomial w (E[w] in LDS), decomposes it into its 2 digit polynomials (rows 2w, 2w+1 of the
+//    TGSW key), runs 2 forward transforms, MACs them with BK_i rows (2w, 2w+1) for BOTH output
+//    polynomials, hands the partial sum of output 1-w to the other wave through LDS, and runs one
+//    inverse transform for output w;
+//  * transform = 512-point complex FFT of the folded polynomial z_n = a_n + i a_{n+512}
+//    evaluated at the 512 roots of X^512 = i (those are roots of X^1024 + 1, so products are
+//    negacyclic): Cooley-Tukey with the twist merged into the twiddles, three radix-8 register
+//    passes (layouts A, B, C: 8 complex per lane) joined by two LDS transposes; the inverse runs
+//    the same network backwards (Gentleman-Sande, conjugate twiddles); the 1/512 scale is folded
+//    into the key.  scripts/emu_v6.py emulates this exact data flow.
+//  * rounding: |coefficient| < 2^52 and the FFT error stays below ~0.05 (emu_v6.py: 0.045 worst
+//    on random keys) << 1/2, so rint() of the result equals the exact product, i.e. the same
+//    integers the exact NTT kernels produce; the mod-2^32 reduction is 3 exact fp64 operations.
+//  * the accumulator E[w] is the periodic negacyclic extension E[k] = +-acc[k mod N],
+//    k < 2240: the rotation X^a reads E[((j - a) mod 2N)] with one base per quarter of the
+//    lane's coefficients and immediate offsets.
+#include <cmath>
+#include <vector>
+#include "engine.h"
+#include "modarith.h"
+
+namespace tfhe_amd {
+
+namespace {
+
+constexpr int kV6Threads = 128;
+constexpr int kExt6 = 2240;          // 2N + 192: quarter bases (< 2N) + 64 * 3
+constexpr int kXSlots = 576;         // 512 complex + pad (slot map of the B <-> C transposes)
+
+struct Cx {
+    double re, im;
+};
+
+struct __attribute__((aligned(16))) V6Shared {
+    double2 X[2][kXSlots];           // per-wave transpose / exchange buffer, 9 KB each
+    uint32_t E[2][kExt6];            // periodic negacyclic accumulator (a, b), 17.5 KB
+    int bara[512];
+    int barb;
+};
+
+struct V6Args {
+    const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
+    const double2 *tw;   // [4] uniform (pass A) + [4][64] (pass B) + [4][64] (pass C)
+};
+
+__device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// (u, v) -> (u + W v, u - W v), W = w (ODD = false) or i w (ODD = true); 6 fp64 ops
+template <bool ODD>
+__device__ __forceinline__ void bf_fwd(Cx &u, Cx &v, const Cx &w) {
+    double xr, xi;
+    if (!ODD) {
+        xr = fma_(w.re, v.re, u.re);
+        xr = fma_(-w.im, v.im, xr);
+        xi = fma_(w.re, v.im, u.im);
+        xi = fma_(w.im, v.re, xi);
+    } else {
+        xr = fma_(-w.re, v.im, u.re);
+        xr = fma_(-w.im, v.re, xr);
+        xi = fma_(w.re, v.re, u.im);
+        xi = fma_(-w.im, v.im, xi);
+    }
+    v.re = fma_(2.0, u.re, -xr);
+    v.im = fma_(2.0, u.im, -xi);
+    u.re = xr;
+    u.im = xi;
+}
+
+// inverse of bf_fwd up to a factor 2: (u, v) -> (u + v, (u - v) conj(W)); 8 fp64 ops
+template <bool ODD>
+__device__ __forceinline__ void bf_inv(Cx &u, Cx &v, const Cx &w) {
+    const double dr = u.re - v.re, di = u.im - v.im;
+    u.re += v.re;
+    u.im += v.im;
+    if (!ODD) {   // d conj(w)
+        v.re = fma_(dr, w.re, di * w.im);
+        v.im = fma_(di, w.re, -(dr * w.im));
+    } else {      // d conj(i w) = -i d conj(w)
+        v.re = fma_(di, w.re, -(dr * w.im));
+        v.im = fma_(-dr, w.re, -(di * w.im));
+    }
+}
+
+// one radix-8 register pass: CT stages at register distance 4, 2, 1
+template <int NP>
+__device__ __forceinline__ void pass_fwd(Cx (&x)[NP][8], const Cx &w0, const Cx &w1, const Cx &w2a, const Cx &w2b) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bf_fwd<false>(x[p][r], x[p][r + 4], w0);
+        bf_fwd<false>(x[p][0], x[p][2], w1);
+        bf_fwd<false>(x[p][1], x[p][3], w1);
+        bf_fwd<true>(x[p][4], x[p][6], w1);
+        bf_fwd<true>(x[p][5], x[p][7], w1);
+        bf_fwd<false>(x[p][0], x[p][1], w2a);
+        bf_fwd<true>(x[p][2], x[p][3], w2a);
+        bf_fwd<false>(x[p][4], x[p][5], w2b);
+        bf_fwd<true>(x[p][6], x[p][7], w2b);
+    }
+}
+
+__device__ __forceinline__ void pass_inv(Cx (&x)[8], const Cx &w0, const Cx &w1, const Cx &w2a, const Cx &w2b) {
+    bf_inv<false>(x[0], x[1], w2a);
+    bf_inv<true>(x[2], x[3], w2a);
+    bf_inv<false>(x[4], x[5], w2b);
+    bf_inv<true>(x[6], x[7], w2b);
+    bf_inv<false>(x[0], x[2], w1);
+    bf_inv<false>(x[1], x[3], w1);
+    bf_inv<true>(x[4], x[6], w1);
+    bf_inv<true>(x[5], x[7], w1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bf_inv<false>(x[r], x[r + 4], w0);
+}
+
+__device__ __forceinline__ Cx ld(const double2 *p) {
+    const double2 v = *p;
+    return Cx{v.x, v.y};
+}
+__device__ __forceinline__ void st(double2 *p, const Cx &v) { *p = make_double2(v.re, v.im); }
+
+// per-lane twiddles of pass B (k = 0) or C (k = 1)
+struct Tw4 {
+    Cx w0, w1, w2a, w2b;
+};
+__device__ __forceinline__ Tw4 load_tw(const double2 *tw, int k, int L) {
+    const double2 *t = tw + 4 + k * 256 + L;
+    return Tw4{ld(t), ld(t + 64), ld(t + 128), ld(t + 192)};
+}
+__device__ __forceinline__ Tw4 load_tw_uniform(const double2 *tw) {
+    return Tw4{ld(tw), ld(tw + 1), ld(tw + 2), ld(tw + 3)};
+}
+
+// Single-wave LDS exchanges: LDS executes one wave's DS instructions in order; the fences
+// keep the compiler from moving a lane's read above another lane's write.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void lds_barrier6() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Slot maps (bank-conflict free for the 16-B accesses):
+//   A <-> B transposes: s(n) = n ^ (8 * bit6(n));  B <-> C: s(n) = n + (n >> 3)
+// layout A: n = L + 64 r;  B: n = (L & 7) + 8 r + 64 (L >> 3);  C: n = 8 L + r
+__device__ __forceinline__ void store_A(double2 *X, const Cx (&x)[8], int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st(X + ((L ^ (8 * (r & 1))) + 64 * r), x[r]);
+}
+__device__ __forceinline__ void load_A(const double2 *X, Cx (&x)[8], int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = ld(X + ((L ^ (8 * (r & 1))) + 64 * r));
+}
+__device__ __forceinline__ int baseB_ab(int L, int odd) {   // slot of (L, r) = base(r & 1) + 8 r
+    const int b = (L >> 3) & 1;
+    const int n0 = (L & 7) + 64 * (L >> 3);
+    return odd ? n0 - 8 * b : n0 + 8 * b;
+}
+__device__ __forceinline__ void load_B_ab(const double2 *X, Cx (&x)[8], int L) {
+    const int e = baseB_ab(L, 0), o = baseB_ab(L, 1);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = ld(X + ((r & 1) ? o : e) + 8 * r);
+}
+__device__ __forceinline__ void store_B_ab(double2 *X, const Cx (&x)[8], int L) {
+    const int e = baseB_ab(L, 0), o = baseB_ab(L, 1);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st(X + ((r & 1) ? o : e) + 8 * r, x[r]);
+}
+__device__ __forceinline__ void store_B_p(double2 *X, const Cx (&x)[8], int L) {
+    const int base = (L & 7) + 72 * (L >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st(X + base + 9 * r, x[r]);
+}
+__device__ __forceinline__ void load_B_p(const double2 *X, Cx (&x)[8], int L) {
+    const int base = (L & 7) + 72 * (L >> 3);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = ld(X + base + 9 * r);
+}
+__device__ __forceinline__ void store_C(double2 *X, const Cx (&x)[8], int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st(X + 9 * L + r, x[r]);
+}
+__device__ __forceinline__ void load_C(const double2 *X, Cx (&x)[8], int L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = ld(X + 9 * L + r);
+}
+
+// forward transform of NP polynomials, layout A in -> layout C out (slot 8 L + r)
+template <int NP>
+__device__ __forceinline__ void fft_fwd(Cx (&x)[NP][8], double2 *X, const double2 *tw, int L) {
+    {
+        const Tw4 t = load_tw_uniform(tw);
+        pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_A(X, x[p], L);
+        wave_sync();
+        load_B_ab(X, x[p], L);
+        wave_sync();
+    }
+    {
+        const Tw4 t = load_tw(tw, 0, L);
+        pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_B_p(X, x[p], L);
+        wave_sync();
+        load_C(X, x[p], L);
+        wave_sync();
+    }
+    {
+        const Tw4 t = load_tw(tw, 1, L);
+        pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
+    }
+}
+
+// the rest of the inverse after pass C: C -> B -> A, natural order out (x 512)
+__device__ __forceinline__ void fft_inv_tail(Cx (&x)[8], double2 *X, const double2 *tw, int L) {
+    store_C(X, x, L);
+    wave_sync();
+    load_B_p(X, x, L);
+    {
+        const Tw4 t = load_tw(tw, 0, L);
+        pass_inv(x, t.w0, t.w1, t.w2a, t.w2b);
+    }
+    wave_sync();
+    store_B_ab(X, x, L);
+    wave_sync();
+    load_A(X, x, L);
+    {
+        const Tw4 t = load_tw_uniform(tw);
+        pass_inv(x, t.w0, t.w1, t.w2a, t.w2b);
+    }
+    wave_sync();
+}
+
+// rint(c) mod 2^32 for |c| < 2^82 (c within 1/2 of an integer): k = c rounded to a multiple
+// of 2^32 by the 1.5*2^84 shifter, then c - k + 1.5*2^52 rounds c - k to an integer in the
+// low mantissa word.  All three operations are exact except the final rounding.
+__device__ __forceinline__ uint32_t torus_of(double c) {
+    constexpr double M1 = 0x1.8p84, M12 = 0x1.8p84 + 0x1.8p52;
+    const double s = c + M1;
+    const double t = s - M12;
+    const double y = c - t;
+    return (uint32_t)__double_as_longlong(y);
+}
+
+__device__ __forceinline__ void e6_store(uint32_t *E, int j, uint32_t v, bool third) {
+    E[j] = v;
+    E[j + kN] = 0u - v;
+    if (third) E[j + 2 * kN] = v;
+}
+
+struct RowTerms6 {
+    int32_t c, sa, sb, sc;
+    const int32_t *xa, *xb, *ya, *yb, *za, *zb;
+};
+
+// one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w
+__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, int i, int a, int w, int L) {
+    uint32_t *E = sh.E[w];
+    double2 *X = sh.X[w];
+    // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
+    // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
+    Cx D[2][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int base = (L + 256 * q - a) & (k2N - 1);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int r = 4 * q + rr;
+            const uint32_t diff = E[base + 64 * rr] - E[L + 64 * r];
+            const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
+            const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
+            if (r < 8) {
+                D[0][r].re = (double)hi;
+                D[1][r].re = (double)lo;
+            } else {
+                D[0][r - 8].im = (double)hi;
+                D[1][r - 8].im = (double)lo;
+            }
+        }
+    }
+    fft_fwd<2>(D, X, g.tw, L);
+    // MAC with rows 2w + p of BK_i for both outputs (layout C, slot 8 L + r)
+    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;   // [p][c][r][L]
+    Cx P[2][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const Cx b0 = ld(bk + (0 * 2 + c) * 512 + r * 64);
+            const Cx b1 = ld(bk + (1 * 2 + c) * 512 + r * 64);
+            double re = D[0][r].re * b0.re;
+            double im = D[0][r].re * b0.im;
+            re = fma_(-D[0][r].im, b0.im, re);
+            im = fma_(D[0][r].im, b0.re, im);
+            re = fma_(D[1][r].re, b1.re, re);
+            im = fma_(D[1][r].re, b1.im, im);
+            re = fma_(-D[1][r].im, b1.im, re);
+            im = fma_(D[1][r].im, b1.re, im);
+            P[c][r] = Cx{re, im};
+        }
+    // partial sums meet: wave w keeps output w, hands output 1 - w over
+    Cx Y[8];
+    if (w == 0) {
+        store_C(X, P[1], L);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) Y[r] = P[0][r];
+    } else {
+        store_C(X, P[0], L);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) Y[r] = P[1][r];
+    }
+    lds_barrier6();
+    {
+        Cx o[8];
+        load_C(sh.X[1 - w], o, L);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            Y[r].re += o[r].re;
+            Y[r].im += o[r].im;
+        }
+    }
+    {
+        const Tw4 t = load_tw(g.tw, 1, L);
+        pass_inv(Y, t.w0, t.w1, t.w2a, t.w2b);
+    }
+    lds_barrier6();   // the other wave has read X[w]
+    fft_inv_tail(Y, X, g.tw, L);
+    // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int j0 = L + 64 * r, j1 = j0 + 512;
+        e6_store(E, j0, E[j0] + torus_of(Y[r].re), r < 3);
+        e6_store(E, j1, E[j1] + torus_of(Y[r].im), false);
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const RowTerms6 &t, int32_t mu,
+                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub) {
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    // gate prologue + modulus switching (lwe-bootstrapping-functions-fft.cu:1851-1858)
+    for (int i = tid; i < kn; i += kV6Threads) {
+        uint32_t x = t.xa ? (uint32_t)t.sa * (uint32_t)t.xa[i] : 0u;
+        if (t.ya) x += (uint32_t)t.sb * (uint32_t)t.ya[i];
+        if (t.za) x += (uint32_t)t.sc * (uint32_t)t.za[i];
+        sh.bara[i] = modswitch_2N(x);
+    }
+    if (tid == 0) {
+        uint32_t xb = (uint32_t)t.c + (t.xb ? (uint32_t)t.sa * (uint32_t)t.xb[0] : 0u);
+        if (t.yb) xb += (uint32_t)t.sb * (uint32_t)t.yb[0];
+        if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
+        sh.barb = modswitch_2N(xb);
+    }
+    __syncthreads();
+    {   // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431), periodic extension
+        const int e = (k2N - sh.barb) & (k2N - 1);
+        for (int k = tid; k < kExt6; k += kV6Threads) {
+            sh.E[0][k] = 0;
+            sh.E[1][k] = ((k - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu;
+        }
+    }
+    __syncthreads();
+    for (int i = 0; i < kn; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
+        cmux_v6(sh, g, i, a, w, L);
+    }
+    __syncthreads();
+    // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
+    for (int j = tid; j < kN; j += kV6Threads) ua[j] = (int32_t)sh.E[0][(k2N - j) & (k2N - 1)];
+    if (tid == 0) *ub = (int32_t)sh.E[1][0];
+}
+
+__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6(V6Args g, int B, BrInput in0, BrInput in1,
+                                                                int32_t mu, int32_t *__restrict__ u_a,
+                                                                int32_t *__restrict__ u_b) {
+    __shared__ V6Shared sh;
+    const int gct = blockIdx.x;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+    RowTerms6 t;
+    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+    t.za = nullptr; t.zb = nullptr;
+    br_v6_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+}
+
+__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_rows(V6Args g, int B, const CircRow *__restrict__ rows,
+                                                                     const int32_t *__restrict__ wa,
+                                                                     const int32_t *__restrict__ wb, int32_t mu,
+                                                                     int32_t *__restrict__ u_a,
+                                                                     int32_t *__restrict__ u_b) {
+    __shared__ V6Shared sh;
+    const int k = blockIdx.x, r = blockIdx.y;
+    const CircRow row = rows[r];
+    auto wire = [&](int wi, const int32_t *&pa, const int32_t *&pb) {
+        if (wi < 0) { pa = nullptr; pb = nullptr; return; }
+        const size_t slot = (size_t)wi * B + k;
+        pa = wa + slot * kn;
+        pb = wb + slot;
+    };
+    RowTerms6 t;
+    t.c = row.c; t.sa = row.sa; t.sb = row.sb; t.sc = row.sc;
+    wire(row.x, t.xa, t.xb);
+    wire(row.y, t.ya, t.yb);
+    wire(row.z, t.za, t.zb);
+    const size_t slot = (size_t)r * B + k;
+    br_v6_body(sh, g, t, mu, u_a + slot * kN, u_b + slot);
+}
+
+__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
+                                                                      const int32_t *__restrict__ bara) {
+    __shared__ V6Shared sh;
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
+    for (int j = tid; j < 2 * kN; j += kV6Threads) {
+        const int c = j >> kLogN, jj = j & (kN - 1);
+        e6_store(sh.E[c], jj, (uint32_t)accg[j], jj < kExt6 - k2N);
+    }
+    for (int i = tid; i < iters; i += kV6Threads) sh.bara[i] = bara[(size_t)blockIdx.x * iters + i] & (k2N - 1);
+    __syncthreads();
+    for (int i = 0; i < iters; ++i) {
+        const int a = sh.bara[i];
+        if (a == 0) continue;
+        cmux_v6(sh, g, i, a, w, L);
+    }
+    __syncthreads();
+    for (int j = tid; j < 2 * kN; j += kV6Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];
+}
+
+// key conversion: one wave per (i, row, c) polynomial; z_n = b_n + i b_{n + 512} -> FFT / 512
+__global__ __launch_bounds__(64) void k_bk_to_fft(const int32_t *__restrict__ bk_coef, double2 *__restrict__ bkf,
+                                                  const double2 *__restrict__ tw) {
+    __shared__ double2 X[kXSlots];
+    const int poly = blockIdx.x;          // (i * 4 + row) * 2 + c, the coefficient layout's order
+    const int L = threadIdx.x;
+    const int32_t *src = bk_coef + (size_t)poly * kN;
+    Cx x[1][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[0][r] = Cx{(double)src[L + 64 * r], (double)src[L + 64 * r + 512]};
+    fft_fwd<1>(x, X, tw, L);
+    double2 *dst = bkf + (size_t)poly * 512 + L;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) st(dst + r * 64, Cx{x[0][r].re * (1.0 / 512), x[0][r].im * (1.0 / 512)});
+}
+
+}  // namespace
+
+// Twiddles of the merged-twist transform (scripts/emu_v6.py twiddles_v6): angles in units of
+// 2 pi / 8192; block b of stage s has modulus X^(2h) - C[s][b]; even blocks take the principal
+// square root, odd blocks i x their even sibling (only even-block twiddles are stored).
+void build_v6_twiddles(double2 *tw) {
+    constexpr int M = 8192;
+    std::vector<int> C{2048};
+    std::vector<std::vector<int>> W;
+    for (int s = 0; s < 9; ++s) {
+        std::vector<int> ws(C.size());
+        for (size_t b = 0; b < C.size(); ++b) ws[b] = (b % 2 == 0) ? C[b] / 2 : (ws[b - 1] + 2048) % M;
+        std::vector<int> nc;
+        for (int x : ws) { nc.push_back(x); nc.push_back((x + M / 2) % M); }
+        W.push_back(ws);
+        C = nc;
+    }
+    auto cis = [&](int e) {
+        const long double th = 2.0L * 3.14159265358979323846264338327950288L * (long double)e / (long double)M;
+        return make_double2((double)cosl(th), (double)sinl(th));
+    };
+    tw[0] = cis(W[0][0]);
+    tw[1] = cis(W[1][0]);
+    tw[2] = cis(W[2][0]);
+    tw[3] = cis(W[2][2]);
+    for (int L = 0; L < 64; ++L) {
+        const int g = L >> 3;
+        tw[4 + 0 * 64 + L] = cis(W[3][g]);
+        tw[4 + 1 * 64 + L] = cis(W[4][2 * g]);
+        tw[4 + 2 * 64 + L] = cis(W[5][4 * g]);
+        tw[4 + 3 * 64 + L] = cis(W[5][4 * g + 2]);
+        tw[4 + 256 + 0 * 64 + L] = cis(W[6][L]);
+        tw[4 + 256 + 1 * 64 + L] = cis(W[7][2 * L]);
+        tw[4 + 256 + 2 * 64 + L] = cis(W[8][4 * L]);
+        tw[4 + 256 + 3 * 64 + L] = cis(W[8][4 * L + 2]);
+    }
+}
+
+hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s) {
+    hipLaunchKernelGGL(k_bk_to_fft, dim3(kn * kKpl * 2), dim3(64), 0, s, d_bk_coef, d_bkf, d_tw);
+    return hipGetLastError();
+}
+
+static V6Args v6_args(const DeviceKey &key) {
+    V6Args g;
+    g.bk = key.bk_fft;
+    g.tw = key.tw6;
+    return g;
+}
+
+hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (!key.bk_fft) return hipErrorInvalidValue;
+    const BrInput in1 = halves > 1 ? in[1] : in[0];
+    hipLaunchKernelGGL(k_blind_rotate_v6, dim3(B * halves), dim3(kV6Threads), 0, s, v6_args(key), B, in[0], in1, mu,
+                       u_a, u_b);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    if (B <= 0 || nrows <= 0) return hipSuccess;
+    if (nrows > 65535 || !key.bk_fft) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_v6_rows, dim3(B, nrows), dim3(kV6Threads), 0, s, v6_args(key), B, rows, wa, wb,
+                       mu, u_a, u_b);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc, const int32_t *bara,
+                                        hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (iters < 0 || iters > kn || !key.bk_fft) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_blind_rotate_v6_debug, dim3(B), dim3(kV6Threads), 0, s, v6_args(key), iters, acc, bara);
+    return hipGetLastError();
+}
+
+}  // namespace tfhe_amd

@@ -334,9 +334,8 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
     const CircLin *d_lin = (const CircLin *)(d_ks + c->ks.size());
     for (const auto &lv : c->levels) {
         if (lv.nrows) {
-            const hipError_t e = use_v5((long)lv.nrows * B)
-                ? launch_blind_rotate_v5_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s)
-                : launch_blind_rotate_v4_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s);
+            const hipError_t e =
+                launch_blind_rotate_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s);
             if (e != hipSuccess) return TFHE_AMD_E_HIP;
             if (launch_keyswitch_rows(key, B, lv.nks, d_ks + lv.ks0, c->u_a, c->u_b, wa, wb, s) != hipSuccess)
                 return TFHE_AMD_E_HIP;

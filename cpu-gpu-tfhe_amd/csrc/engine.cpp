@@ -75,24 +75,10 @@ int br_version() {
     if (v < 0) {
         const char *e = getenv("TFHE_AMD_BR");
         v = e ? atoi(e) : 0;
-        if (v < 0 || v > 5) v = 0;
+        if (v < 0 || v > 6) v = 0;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
-}
-
-// auto mode: the latency kernel (8 waves per ciphertext, one per CU) while a launch has few
-// ciphertexts; the throughput kernel (2 waves, 4 per CU) once it fills the chip
-static long v5_threshold() {
-    static const long t = [] {
-        const char *e = getenv("TFHE_AMD_V5_MAX");
-        return e ? atol(e) : 512L;
-    }();
-    return t;
-}
-bool use_v5(long count) {
-    const int v = br_version();
-    return v == 5 || (v == 0 && count <= v5_threshold());
 }
 
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
@@ -103,9 +89,17 @@ static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput 
     case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
     case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
-    default:
-        return use_v5((long)B * halves) ? launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s)
-                                        : launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
+    case 6: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
+    default: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
+    }
+}
+
+hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+    switch (br_version()) {
+    case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+    case 5: return launch_blind_rotate_v5_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+    default: return launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     }
 }
 
@@ -150,6 +144,8 @@ static int free_key(DeviceKey &k) {
     if (k.device >= 0) (void)hipSetDevice(k.device);
     if (k.bk_ntt) (void)hipFree(k.bk_ntt);
     if (k.bk_v2) (void)hipFree(k.bk_v2);
+    if (k.bk_fft) (void)hipFree(k.bk_fft);
+    if (k.tw6) (void)hipFree(k.tw6);
     if (k.tw2) (void)hipFree(k.tw2);
     if (k.tw4) (void)hipFree(k.tw4);
     if (k.ksk) (void)hipFree(k.ksk);
@@ -214,6 +210,10 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         build_v4_twiddles(*ht, tw4.data(), tw4.data() + 32, tw4.data() + 32 + 2 * 27 * 64);
         HIPCHK(hipMalloc(&c->key.tw4, sizeof(uint2) * tw4.size()));
         HIPCHK(hipMemcpy(c->key.tw4, tw4.data(), sizeof(uint2) * tw4.size(), hipMemcpyHostToDevice));
+        std::vector<double2> tw6(kTw6Words);
+        build_v6_twiddles(tw6.data());
+        HIPCHK(hipMalloc(&c->key.tw6, sizeof(double2) * tw6.size()));
+        HIPCHK(hipMemcpy(c->key.tw6, tw6.data(), sizeof(double2) * tw6.size(), hipMemcpyHostToDevice));
     }
     delete ht;
 
@@ -226,6 +226,8 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         HIPCHK(launch_bk_to_ntt(d_coef, c->key.bk_ntt, c->key.tables, c->stream));
         HIPCHK(hipMalloc(&c->key.bk_v2, sizeof(uint32_t) * 2 * coef_words));
         HIPCHK(launch_bk_v1_to_v2(c->key.bk_ntt, c->key.bk_v2, c->stream));
+        HIPCHK(hipMalloc(&c->key.bk_fft, sizeof(double2) * (size_t)kn * kKpl * 2 * 512));
+        HIPCHK(launch_bk_to_fft(d_coef, c->key.bk_fft, c->key.tw6, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(d_coef));
         c->key.has_bk = true;
@@ -461,7 +463,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
            : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
            : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
-                    : launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s));   // v5 shares v4's math
+           : (v == 4 || v == 5) ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)   // v5 shares v4's math
+                    : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
 
@@ -579,19 +582,20 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version < 0 || br_version > 5) return TFHE_AMD_E_ARG;
+    if (br_version < 0 || br_version > 6) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }
 
 extern "C" const char *tfhe_amd_version(void) {
     // one immutable string per (blind-rotation, key-switch) generation pair
-    static char names[6][5][48];
+    static char names[7][5][48];
     static std::once_flag once;
     std::call_once(once, [] {
-        for (int b = 0; b <= 5; b++)
+        for (int b = 0; b <= 6; b++)
             for (int k = 1; k <= 4; k++) {
-                if (b == 0) snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v4v5 ks-v%d", k);
+                if (b == 0 || b == 6)
+                    snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v6 ks-v%d", k);
                 else snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
             }
     });

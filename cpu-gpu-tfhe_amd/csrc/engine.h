@@ -14,6 +14,8 @@ struct DeviceKey {
     uint32_t *bk_v2 = nullptr;    // v2: [kn][2 primes][2 c][kKpl][4 v][64 L][4 e] (same values)
     uint2 *tw2 = nullptr;         // v2 twiddles: uniform fwd/inv [2][16] x2, streams [2][27][64], [2][18][64]
     uint2 *tw4 = nullptr;         // v4 inverse-CT twiddles: uniform [2][16], streams [2][27][64], post-twist [2][16][64]
+    double2 *bk_fft = nullptr;    // v6: [kn][4 rows][2 c][8 r][64 L] FFT-domain key / 512 (slot 8 L + r)
+    double2 *tw6 = nullptr;       // v6 twiddles: [4] uniform + [4][64] pass B + [4][64] pass C
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     int32_t *ksk4 = nullptr;      // ks-v4: [126 column blocks][kN][kKsT][3][4]
     NttTables *tables = nullptr;  // device copy
@@ -23,6 +25,7 @@ struct DeviceKey {
 };
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
+constexpr int kTw6Words = 4 + 2 * 4 * 64;   // double2 entries
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -81,10 +84,20 @@ hipError_t launch_blind_rotate_v5(const DeviceKey &key, int B, int halves, const
                                   int32_t *u_a, int32_t *u_b, hipStream_t s);
 hipError_t launch_blind_rotate_v5_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
-// v4 vs v5 for `count` blind rotations in one launch (br_version 0 = auto)
-bool use_v5(long count);
-// which blind-rotation kernel runs: 0 = auto (v5 for small launches, v4 otherwise), 1..5 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
+// v6 (fp64 FFT external product, the reference's arithmetic), blind_rotate_v6.hip
+void build_v6_twiddles(double2 *tw);
+hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s);
+hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                        const int32_t *bara, hipStream_t s);
+// which blind-rotation kernel runs: 0 = default (v6), 1..6 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
+// circuit level blind rotation with the selected kernel (rows variants of v4 / v5 / v6)
+hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
 
 // which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)
 int ks_version();

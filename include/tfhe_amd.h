@@ -130,15 +130,16 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 /* TLWE secret key (int32 [1024]; k = 1), = the extracted LWE key of woKS outputs */
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
-/* Select the blind-rotation kernel generation: 0 = auto (the default: v5 for launches of at
- * most TFHE_AMD_V5_MAX = 512 blind rotations, v4 above), 1 = LDS radix-2 reference kernel,
- * 2 = register-resident NTT with 2 waves per ciphertext, 3 = 4 waves per ciphertext,
- * 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT and a periodic accumulator (throughput),
- * 5 = 8 waves per ciphertext (latency); env TFHE_AMD_BR=<n> does the same at startup.
- * For A/B measurements and parity cross-checks; results are identical by contract. */
+/* Select the blind-rotation kernel generation: 0 = default (v6), 1..5 = exact 2-prime NTT
+ * kernels (1 = LDS radix-2 reference kernel, 2 = register-resident NTT with 2 waves per
+ * ciphertext, 3 = 4 waves per ciphertext, 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT
+ * and a periodic accumulator, 5 = 8 waves per ciphertext), 6 = fp64 FFT external product (the
+ * reference's arithmetic; its rounded products equal the exact ones: FFT error < 0.05 << 1/2).
+ * env TFHE_AMD_BR=<n> does the same at startup.  For A/B measurements and parity
+ * cross-checks; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
 
-/* build tag, e.g. "tfhe_amd gfx950 ntt2x30 br-v1" */
+/* build tag, e.g. "tfhe_amd gfx950 fft64 br-v6 ks-v4" */
 const char *tfhe_amd_version(void);
 
 /* ---------------------------------------------------------------- circuits (§8(f) row 1)
