@@ -34,6 +34,9 @@ namespace tfhe_amd {
 namespace {
 
 constexpr int kV6Threads = 128;
+#ifndef TFHE_AMD_V6_WAVES
+#define TFHE_AMD_V6_WAVES 2          // waves per SIMD the register allocation targets
+#endif
 constexpr int kExt6 = 2240;          // 2N + 192: quarter bases (< 2N) + 64 * 3
 constexpr int kXSlots = 576;         // 512 complex + pad (slot map of the B <-> C transposes)
 
@@ -41,12 +44,29 @@ struct Cx {
     double re, im;
 };
 
+#ifdef TFHE_AMD_V6_STAMPS
+// phase timing diagnostics: cumulative shader-clock cycles per phase of waves 0 and 1 of
+// workgroup 0 (lane 0); read with tfhe_amd_debug_v6_stamps (scripts/v6_stamps.py)
+__device__ unsigned long long g_v6_stamps[2][12];
+__device__ unsigned long long g_v6_tprev[2];
+#define V6_STAMP(k)                                                              \
+    do {                                                                          \
+        if (blockIdx.x == 0 && blockIdx.y == 0 && L == 0) {                       \
+            const unsigned long long now = __builtin_amdgcn_s_memtime();          \
+            g_v6_stamps[w][k] += now - g_v6_tprev[w];                             \
+            g_v6_tprev[w] = now;                                                  \
+        }                                                                         \
+    } while (0)
+#else
+#define V6_STAMP(k) do {} while (0)
+#endif
+
 struct __attribute__((aligned(16))) V6Shared {
-    double2 X[2][kXSlots];           // per-wave transpose / exchange buffer, 9 KB each
-    uint32_t E[2][kExt6];            // periodic negacyclic accumulator (a, b), 17.5 KB
-    int bara[512];
+    double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
+    short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
 };
+static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave buffer");
 
 struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
@@ -196,22 +216,37 @@ __device__ __forceinline__ void load_C(const double2 *X, Cx (&x)[8], int L) {
     for (int r = 0; r < 8; ++r) x[r] = ld(X + 9 * L + r);
 }
 
-// forward transform of NP polynomials, layout A in -> layout C out (slot 8 L + r)
+// wave-uniform double -> SGPR pair
+__device__ __forceinline__ double uni(double v) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)bits);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(bits >> 32));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ Tw4 load_tw_sgpr(const double2 *tw) {
+    Tw4 t = load_tw_uniform(tw);
+    t.w0 = Cx{uni(t.w0.re), uni(t.w0.im)};
+    t.w1 = Cx{uni(t.w1.re), uni(t.w1.im)};
+    t.w2a = Cx{uni(t.w2a.re), uni(t.w2a.im)};
+    t.w2b = Cx{uni(t.w2b.re), uni(t.w2b.im)};
+    return t;
+}
+
+// forward transform of NP polynomials, layout A in -> layout C (slot 8 L + r): passes A and
+// B and both transposes; the caller runs pass C (fft_fwd_C) so that it can put loads in
+// flight first.  tA = the pass-A (uniform) twiddles, held in SGPRs for the whole kernel.
 template <int NP>
-__device__ __forceinline__ void fft_fwd(Cx (&x)[NP][8], double2 *X, const double2 *tw, int L) {
+__device__ __forceinline__ void fft_fwd_AB(Cx (&x)[NP][8], double2 *X, const double2 *tw, const Tw4 &tA, int L) {
+    pass_fwd<NP>(x, tA.w0, tA.w1, tA.w2a, tA.w2b);
     {
-        const Tw4 t = load_tw_uniform(tw);
-        pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
-    }
+        const Tw4 t = load_tw(tw, 0, L);   // in flight during the transpose
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        store_A(X, x[p], L);
-        wave_sync();
-        load_B_ab(X, x[p], L);
-        wave_sync();
-    }
-    {
-        const Tw4 t = load_tw(tw, 0, L);
+        for (int p = 0; p < NP; ++p) {
+            store_A(X, x[p], L);
+            wave_sync();
+            load_B_ab(X, x[p], L);
+            wave_sync();
+        }
         pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
     }
 #pragma unroll
@@ -221,30 +256,10 @@ __device__ __forceinline__ void fft_fwd(Cx (&x)[NP][8], double2 *X, const double
         load_C(X, x[p], L);
         wave_sync();
     }
-    {
-        const Tw4 t = load_tw(tw, 1, L);
-        pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
-    }
 }
-
-// the rest of the inverse after pass C: C -> B -> A, natural order out (x 512)
-__device__ __forceinline__ void fft_inv_tail(Cx (&x)[8], double2 *X, const double2 *tw, int L) {
-    store_C(X, x, L);
-    wave_sync();
-    load_B_p(X, x, L);
-    {
-        const Tw4 t = load_tw(tw, 0, L);
-        pass_inv(x, t.w0, t.w1, t.w2a, t.w2b);
-    }
-    wave_sync();
-    store_B_ab(X, x, L);
-    wave_sync();
-    load_A(X, x, L);
-    {
-        const Tw4 t = load_tw_uniform(tw);
-        pass_inv(x, t.w0, t.w1, t.w2a, t.w2b);
-    }
-    wave_sync();
+template <int NP>
+__device__ __forceinline__ void fft_fwd_C(Cx (&x)[NP][8], const Tw4 &tC) {
+    pass_fwd<NP>(x, tC.w0, tC.w1, tC.w2a, tC.w2b);
 }
 
 // rint(c) mod 2^32 for |c| < 2^82 (c within 1/2 of an integer): k = c rounded to a multiple
@@ -264,15 +279,53 @@ __device__ __forceinline__ void e6_store(uint32_t *E, int j, uint32_t v, bool th
     if (third) E[j + 2 * kN] = v;
 }
 
+// the accumulator polynomial of this wave, coefficient L + 64 r in acc[r], written as its
+// periodic negacyclic extension E[k] = +-acc[k mod N] (k < 2240) into the wave's buffer
+__device__ __forceinline__ void write_ext(uint32_t *E, const uint32_t (&acc)[16], int L) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) e6_store(E, L + 64 * r, acc[r], r < 3);
+}
+
+// BK_i rows 2w, 2w + 1 of output c for this lane: 16 x 16 B, all in flight together
+__device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        b[0][r] = ld(bk + c * 512 + r * 64);
+        b[1][r] = ld(bk + (2 + c) * 512 + r * 64);
+    }
+}
+// Y = D_0 (x) BK[row 2w][c] + D_1 (x) BK[row 2w + 1][c], layout C
+__device__ __forceinline__ void mac6(const Cx (&D)[2][8], const Cx (&b)[2][8], Cx (&Y)[8]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const Cx &b0 = b[0][r], &b1 = b[1][r];
+        double re = D[0][r].re * b0.re;
+        double im = D[0][r].re * b0.im;
+        re = fma_(-D[0][r].im, b0.im, re);
+        im = fma_(D[0][r].im, b0.re, im);
+        re = fma_(D[1][r].re, b1.re, re);
+        im = fma_(D[1][r].re, b1.im, im);
+        re = fma_(-D[1][r].im, b1.im, re);
+        im = fma_(D[1][r].im, b1.re, im);
+        Y[r] = Cx{re, im};
+    }
+}
+
 struct RowTerms6 {
     int32_t c, sa, sb, sc;
     const int32_t *xa, *xb, *ya, *yb, *za, *zb;
 };
 
-// one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w
-__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, int i, int a, int w, int L) {
-    uint32_t *E = sh.E[w];
+// one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
+// accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
+// (rotation reads), the FFT transposes and the partial sum handed to the other wave.
+__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int L,
+                                        uint32_t (&acc)[16]) {
     double2 *X = sh.X[w];
+    uint32_t *E = reinterpret_cast<uint32_t *>(X);
+    V6_STAMP(9);
+    write_ext(E, acc, L);
+    wave_sync();
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
     Cx D[2][8];
@@ -282,7 +335,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, int i, in
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             const int r = 4 * q + rr;
-            const uint32_t diff = E[base + 64 * rr] - E[L + 64 * r];
+            const uint32_t diff = E[base + 64 * rr] - acc[r];
             const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
             const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
             if (r < 8) {
@@ -294,38 +347,29 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, int i, in
             }
         }
     }
-    fft_fwd<2>(D, X, g.tw, L);
-    // MAC with rows 2w + p of BK_i for both outputs (layout C, slot 8 L + r)
-    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;   // [p][c][r][L]
-    Cx P[2][8];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const Cx b0 = ld(bk + (0 * 2 + c) * 512 + r * 64);
-            const Cx b1 = ld(bk + (1 * 2 + c) * 512 + r * 64);
-            double re = D[0][r].re * b0.re;
-            double im = D[0][r].re * b0.im;
-            re = fma_(-D[0][r].im, b0.im, re);
-            im = fma_(D[0][r].im, b0.re, im);
-            re = fma_(D[1][r].re, b1.re, re);
-            im = fma_(D[1][r].re, b1.im, im);
-            re = fma_(-D[1][r].im, b1.im, re);
-            im = fma_(D[1][r].im, b1.re, im);
-            P[c][r] = Cx{re, im};
-        }
-    // partial sums meet: wave w keeps output w, hands output 1 - w over
+    wave_sync();
+    V6_STAMP(0);
+    fft_fwd_AB<2>(D, X, g.tw, tA, L);
+    V6_STAMP(1);
+    // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
+    // to the other wave through this wave's buffer, then output w.  The first key slice is in
+    // flight during pass C, the second during the first MAC and the hand-over store.
+    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
+    Cx bv[2][8];
+    const Tw4 tC = load_tw(g.tw, 1, L);
+    load_bk(bv, bk, 1 - w);
+    __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
+    fft_fwd_C<2>(D, tC);
     Cx Y[8];
-    if (w == 0) {
-        store_C(X, P[1], L);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) Y[r] = P[0][r];
-    } else {
-        store_C(X, P[0], L);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) Y[r] = P[1][r];
-    }
+    mac6(D, bv, Y);
+    V6_STAMP(2);
+    load_bk(bv, bk, w);
+    __builtin_amdgcn_sched_barrier(0);
+    store_C(X, Y, L);
+    mac6(D, bv, Y);
+    V6_STAMP(3);
     lds_barrier6();
+    V6_STAMP(4);
     {
         Cx o[8];
         load_C(sh.X[1 - w], o, L);
@@ -339,16 +383,28 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, int i, in
         const Tw4 t = load_tw(g.tw, 1, L);
         pass_inv(Y, t.w0, t.w1, t.w2a, t.w2b);
     }
+    const Tw4 tB = load_tw(g.tw, 0, L);
+    V6_STAMP(5);
     lds_barrier6();   // the other wave has read X[w]
-    fft_inv_tail(Y, X, g.tw, L);
+    V6_STAMP(6);
+    store_C(X, Y, L);
+    wave_sync();
+    load_B_p(X, Y, L);
+    pass_inv(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
+    wave_sync();
+    store_B_ab(X, Y, L);
+    wave_sync();
+    load_A(X, Y, L);
+    pass_inv(Y, tA.w0, tA.w1, tA.w2a, tA.w2b);
+    V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im)
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        const int j0 = L + 64 * r, j1 = j0 + 512;
-        e6_store(E, j0, E[j0] + torus_of(Y[r].re), r < 3);
-        e6_store(E, j1, E[j1] + torus_of(Y[r].im), false);
+        acc[r] += torus_of(Y[r].re);
+        acc[r + 8] += torus_of(Y[r].im);
     }
     wave_sync();
+    V6_STAMP(8);
 }
 
 __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const RowTerms6 &t, int32_t mu,
@@ -361,7 +417,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         uint32_t x = t.xa ? (uint32_t)t.sa * (uint32_t)t.xa[i] : 0u;
         if (t.ya) x += (uint32_t)t.sb * (uint32_t)t.ya[i];
         if (t.za) x += (uint32_t)t.sc * (uint32_t)t.za[i];
-        sh.bara[i] = modswitch_2N(x);
+        sh.bara[i] = (short)modswitch_2N(x);
     }
     if (tid == 0) {
         uint32_t xb = (uint32_t)t.c + (t.xb ? (uint32_t)t.sa * (uint32_t)t.xb[0] : 0u);
@@ -369,27 +425,37 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
+    const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
-    {   // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431), periodic extension
+    // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
+    uint32_t acc[16];
+    {
         const int e = (k2N - sh.barb) & (k2N - 1);
-        for (int k = tid; k < kExt6; k += kV6Threads) {
-            sh.E[0][k] = 0;
-            sh.E[1][k] = ((k - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu;
-        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            acc[r] = w == 0 ? 0u : (((L + 64 * r - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu);
     }
-    __syncthreads();
     for (int i = 0; i < kn; ++i) {
         const int a = sh.bara[i];
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6(sh, g, i, a, w, L);
+        cmux_v6(sh, g, tA, i, a, w, L, acc);
     }
-    __syncthreads();
     // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
-    for (int j = tid; j < kN; j += kV6Threads) ua[j] = (int32_t)sh.E[0][(k2N - j) & (k2N - 1)];
-    if (tid == 0) *ub = (int32_t)sh.E[1][0];
+    if (w == 0) {
+        uint32_t *E = reinterpret_cast<uint32_t *>(sh.X[0]);
+        write_ext(E, acc, L);
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int j = L + 64 * r;
+            ua[j] = (int32_t)E[(k2N - j) & (k2N - 1)];
+        }
+    } else if (L == 0) {
+        *ub = (int32_t)acc[0];
+    }
 }
 
-__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6(V6Args g, int B, BrInput in0, BrInput in1,
+__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6(V6Args g, int B, BrInput in0, BrInput in1,
                                                                 int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
     __shared__ V6Shared sh;
@@ -405,7 +471,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6(V6Args g, int
     br_v6_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
 }
 
-__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_rows(V6Args g, int B, const CircRow *__restrict__ rows,
+__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, const CircRow *__restrict__ rows,
                                                                      const int32_t *__restrict__ wa,
                                                                      const int32_t *__restrict__ wb, int32_t mu,
                                                                      int32_t *__restrict__ u_a,
@@ -428,26 +494,26 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_rows(V6Args g
     br_v6_body(sh, g, t, mu, u_a + slot * kN, u_b + slot);
 }
 
-__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
+__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
                                                                       const int32_t *__restrict__ bara) {
     __shared__ V6Shared sh;
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
-    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
-    for (int j = tid; j < 2 * kN; j += kV6Threads) {
-        const int c = j >> kLogN, jj = j & (kN - 1);
-        e6_store(sh.E[c], jj, (uint32_t)accg[j], jj < kExt6 - k2N);
-    }
-    for (int i = tid; i < iters; i += kV6Threads) sh.bara[i] = bara[(size_t)blockIdx.x * iters + i] & (k2N - 1);
+    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN + (size_t)w * kN;
+    uint32_t ac[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ac[r] = (uint32_t)accg[L + 64 * r];
+    for (int i = tid; i < iters; i += kV6Threads) sh.bara[i] = (short)(bara[(size_t)blockIdx.x * iters + i] & (k2N - 1));
+    const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     for (int i = 0; i < iters; ++i) {
         const int a = sh.bara[i];
         if (a == 0) continue;
-        cmux_v6(sh, g, i, a, w, L);
+        cmux_v6(sh, g, tA, i, a, w, L, ac);
     }
-    __syncthreads();
-    for (int j = tid; j < 2 * kN; j += kV6Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];
 }
 
 // key conversion: one wave per (i, row, c) polynomial; z_n = b_n + i b_{n + 512} -> FFT / 512
@@ -460,7 +526,8 @@ __global__ __launch_bounds__(64) void k_bk_to_fft(const int32_t *__restrict__ bk
     Cx x[1][8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) x[0][r] = Cx{(double)src[L + 64 * r], (double)src[L + 64 * r + 512]};
-    fft_fwd<1>(x, X, tw, L);
+    fft_fwd_AB<1>(x, X, tw, load_tw_sgpr(tw), L);
+    fft_fwd_C<1>(x, load_tw(tw, 1, L));
     double2 *dst = bkf + (size_t)poly * 512 + L;
 #pragma unroll
     for (int r = 0; r < 8; ++r) st(dst + r * 64, Cx{x[0][r].re * (1.0 / 512), x[0][r].im * (1.0 / 512)});
@@ -544,3 +611,16 @@ hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, 
 }
 
 }  // namespace tfhe_amd
+
+#ifdef TFHE_AMD_V6_STAMPS
+extern "C" int tfhe_amd_debug_v6_stamps(unsigned long long *out, int reset) {
+    unsigned long long h[24];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(tfhe_amd::g_v6_stamps), sizeof h) != hipSuccess) return -2;
+    for (int i = 0; i < 24; i++) out[i] = h[i];
+    if (reset) {
+        unsigned long long z[24] = {0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(tfhe_amd::g_v6_stamps), z, sizeof z);
+    }
+    return 0;
+}
+#endif

@@ -4,7 +4,7 @@ set -u
 for b in $1; do
   for v in $2; do
     TFHE_AMD_BR=$v timeout -k 10 300 python bench.py --steps 3 --warmup 1 --batch $b --no-cpu-baseline > gpurun_out/sw_${v}_${b}.log 2>&1
-    rc=$?; [ $rc -ge 124 ] && exit $rc
+    rc=$?; [ $rc -ne 0 ] && exit $rc
     python3 - "$v" "$b" <<'PY'
 import json, sys
 v, b = sys.argv[1], sys.argv[2]
