@@ -9,15 +9,15 @@ rank processes its own shard of independent ciphertexts; no collective on the da
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
 Rank 0 prints ONE JSON line.  Extra objects:
-  roofline     : the dominant kernel = the blind rotation (k_blind_rotate_v6, fp64 FFT external
-                 product).  It is bound by fp64 VALU issue, not HBM (the 32.8 MB key stream per
-                 bootstrap is shared by the whole batch and served from L2/MALL: PMC traffic is
-                 ~2.5 % of it), so `achieved` = its algorithmic fp64 FLOPs (193 536 per CMux
-                 step x 500 steps per bootstrap x B; FMA = 2) / its average launch time (HIP
-                 events on the stream it runs on) vs the 78.6 TFLOP/s fp64 vector peak; traffic
-                 = HBM bytes per launch from the profiles/ PMC data.  The key-stream rate is
-                 reported beside it (`key_stream_GBps`).  With an exact-NTT kernel pinned
-                 (TFHE_AMD_BR=1..5) the line falls back to the key-stream / HBM framing.
+  roofline     : SURVEY.md §8(d)'s figure for the dominant kernel (the blind rotation): its
+                 algorithmic key-stream bytes (32 768 000 B of TGSW key per bootstrap, NTT or
+                 FFT domain alike) / its average launch time (HIP events on the stream it runs
+                 on) vs the 8 TB/s HBM peak; `traffic` = the HBM bytes per launch from the
+                 profiles/ PMC data.  Every ciphertext of the batch streams the same key slice
+                 per step, so the reads are L2/MALL hits and `frac` can exceed 1; the kernel is
+                 in fact bound by fp64 VALU issue, which `roofline.compute` reports: its
+                 algorithmic fp64 FLOPs (198 656 per CMux step, FMA = 2) / launch time vs the
+                 78.6 TFLOP/s fp64 vector peak.
   cpu_baseline : the CPU restatement (oracle/, same algorithm, exact NTT, OpenMP) timed on
                  this host's cores on a bounded sample of the same workload (rank 0, N=1).
 """
@@ -35,10 +35,11 @@ sys.path.insert(0, os.path.join(REPO, "cpu-gpu-tfhe_amd"))
 BK_BYTES_PER_BOOTSTRAP = 500 * 4 * 2 * 1024 * 8        # NTT-domain TGSW key stream, 32 768 000 B
 KS_BYTES_PER_KEYSWITCH = 1024 * 8 * 501 * 4            # KSK rows, 16 416 768 B
 HBM_PEAK_GBPS = 8000.0
-# v6 fp64 work per CMux step (blind_rotate_v6.hip): 4 forward transforms x 2304
-# butterflies x 12 + 2 inverse x 2304 x 10 + MAC 2 x 4 x 512 x 7 + partial sums 2048 +
-# mod-2^32 rounding 2048 x 3
-FLOPS_PER_CMUX = 4 * 2304 * 12 + 2 * 2304 * 10 + 2 * 4 * 512 * 7 + 2048 + 2048 * 3   # 193 536
+# v6 fp64 work per CMux step (blind_rotate_v6.hip), FMA = 2: 4 forward
+# transforms x 2304 butterflies x 12 + 2 inverse (640 trivial butterflies x 4 + 1664 x 12 +
+# 512-point post-twist x 6) + MAC 2 x 4 x 512 x 7 + partial sums 2048 + mod-2^32 rounding 2048 x 3
+INV_FLOPS = 640 * 4 + 1664 * 12 + 512 * 6
+FLOPS_PER_CMUX = 4 * 2304 * 12 + 2 * INV_FLOPS + 2 * 4 * 512 * 7 + 2048 + 2048 * 3   # 198 656
 FLOPS_PER_BOOTSTRAP = 500 * FLOPS_PER_CMUX
 FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP), AMD spec
 
@@ -164,17 +165,15 @@ def main():
     ks_ms = prof["ks_ms"] / max(1, prof["ks_launches"])
     key_gbps = B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9
     fft = "fft64" in T.version()
+    roof = {"bound": "hbm", "achieved": key_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": key_gbps / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
+            "kernel": "k_blind_rotate_v6" if fft else "k_blind_rotate", "kernel_ms": br_ms,
+            "keyswitch_ms": ks_ms, "algorithmic_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP}
     if fft:
-        achieved = B * FLOPS_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e12
-        roof = {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(T.version(), B),
-                "kernel": "k_blind_rotate_v6", "dtype": "f64", "flops_per_launch": B * FLOPS_PER_BOOTSTRAP}
-    else:
-        roof = {"bound": "hbm", "achieved": key_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": key_gbps / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
-                "kernel": "k_blind_rotate"}
-    roof.update({"kernel_ms": br_ms, "keyswitch_ms": ks_ms, "key_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP,
-                 "key_stream_GBps": key_gbps})
+        tflops = B * FLOPS_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e12
+        roof["compute"] = {"bound": "valu-fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": tflops / FP64_PEAK_TFLOPS,
+                           "flops_per_launch": B * FLOPS_PER_BOOTSTRAP}
 
     value = shard.weak_scaling_value(B, world, args.steps, elapsed)
     line = {

@@ -7,23 +7,25 @@
 // per prime, where the fp64 butterfly below costs 6 full-rate v_fma_f64 (MI355X: fp64 vector
 // FMA at the fp32 rate), so v6 returns to the reference's arithmetic, MI355X-shaped:
 //
-//  * one ciphertext = 2 waves (128 threads, 4 workgroups per CU); wave w owns accumulator
-//    polynomial w (E[w] in LDS), decomposes it into its 2 digit polynomials (rows 2w, 2w+1 of the
-//    TGSW key), runs 2 forward transforms, MACs them with BK_i rows (2w, 2w+1) for BOTH output
-//    polynomials, hands the partial sum of output 1-w to the other wave through LDS, and runs one
-//    inverse transform for output w;
+//  * one ciphertext = 2 waves (128 threads); wave w owns accumulator polynomial w (16 Torus32
+//    coefficients per lane, in registers), decomposes it into its 2 digit polynomials (rows 2w,
+//    2w+1 of the TGSW key), runs 2 forward transforms, MACs them with BK_i rows (2w, 2w+1) for
+//    BOTH output polynomials, hands the partial sum of output 1-w to the other wave through LDS,
+//    and runs one inverse transform for output w;
 //  * transform = 512-point complex FFT of the folded polynomial z_n = a_n + i a_{n+512}
 //    evaluated at the 512 roots of X^512 = i (those are roots of X^1024 + 1, so products are
 //    negacyclic): Cooley-Tukey with the twist merged into the twiddles, three radix-8 register
-//    passes (layouts A, B, C: 8 complex per lane) joined by two LDS transposes; the inverse runs
-//    the same network backwards (Gentleman-Sande, conjugate twiddles); the 1/512 scale is folded
-//    into the key.  scripts/emu_v6.py emulates this exact data flow.
+//    passes (layouts A, B, C: 8 complex per lane) joined by two LDS transposes.  Its output is
+//    in bit-reversed order of zeta omega^k, so the inverse is a radix-2 DIT on that order
+//    (constant twiddles in pass C, per-lane ones in passes B and A) plus a zeta^-n post-twist;
+//    the 1/512 scale is folded into the key.  scripts/emu_v6.py emulates this exact data flow.
 //  * rounding: |coefficient| < 2^52 and the FFT error stays below ~0.05 (emu_v6.py: 0.045 worst
 //    on random keys) << 1/2, so rint() of the result equals the exact product, i.e. the same
 //    integers the exact NTT kernels produce; the mod-2^32 reduction is 3 exact fp64 operations.
-//  * the accumulator E[w] is the periodic negacyclic extension E[k] = +-acc[k mod N],
-//    k < 2240: the rotation X^a reads E[((j - a) mod 2N)] with one base per quarter of the
-//    lane's coefficients and immediate offsets.
+//  * each wave has ONE 9 KB LDS buffer: per step it holds the periodic negacyclic extension
+//    E[k] = +-acc[k mod N] (k < 2240: the rotation X^a reads E[(j - a) mod 2N] with one base per
+//    quarter of the lane's coefficients), then the FFT transposes, then the partial sum handed
+//    to the other wave (19.5 KB per ciphertext).
 #include <cmath>
 #include <vector>
 #include "engine.h"
@@ -34,9 +36,10 @@ namespace tfhe_amd {
 namespace {
 
 constexpr int kV6Threads = 128;
-#ifndef TFHE_AMD_V6_WAVES
-#define TFHE_AMD_V6_WAVES 2          // waves per SIMD the register allocation targets
-#endif
+// Register budget: 2 waves per SIMD (256 VGPRs; 16 key loads in flight).  A 1024-ciphertext
+// launch has exactly 2 waves per SIMD, and 3- or 4-wave budgets (8 loads in flight, <= 168 or
+// 128 VGPRs) measured slower at every batch size (B = 2048: 8.4 -> 16.6 ms).
+constexpr int kV6Waves = 2;
 constexpr int kExt6 = 2240;          // 2N + 192: quarter bases (< 2N) + 64 * 3
 constexpr int kXSlots = 576;         // 512 complex + pad (slot map of the B <-> C transposes)
 
@@ -45,20 +48,26 @@ struct Cx {
 };
 
 #ifdef TFHE_AMD_V6_STAMPS
-// phase timing diagnostics: cumulative shader-clock cycles per phase of waves 0 and 1 of
-// workgroup 0 (lane 0); read with tfhe_amd_debug_v6_stamps (scripts/v6_stamps.py)
+// phase timing diagnostics: shader-clock cycles per phase, accumulated in (uniform) registers
+// and written by waves 0 and 1 of workgroup 0 at the end; read with tfhe_amd_debug_v6_stamps
+// (scripts/v6_stamps.py)
 __device__ unsigned long long g_v6_stamps[2][12];
-__device__ unsigned long long g_v6_tprev[2];
-#define V6_STAMP(k)                                                              \
-    do {                                                                          \
-        if (blockIdx.x == 0 && blockIdx.y == 0 && L == 0) {                       \
-            const unsigned long long now = __builtin_amdgcn_s_memtime();          \
-            g_v6_stamps[w][k] += now - g_v6_tprev[w];                             \
-            g_v6_tprev[w] = now;                                                  \
-        }                                                                         \
+struct V6Stamps {
+    unsigned long long acc[10] = {0};
+    unsigned long long prev = 0;
+};
+#define V6_STAMP(k)                                                 \
+    do {                                                             \
+        const unsigned long long now = __builtin_amdgcn_s_memtime(); \
+        stamps.acc[k] += now - stamps.prev;                          \
+        stamps.prev = now;                                           \
     } while (0)
+#define V6_STAMPS_PARAM , V6Stamps &stamps
+#define V6_STAMPS_ARG , stamps
 #else
 #define V6_STAMP(k) do {} while (0)
+#define V6_STAMPS_PARAM
+#define V6_STAMPS_ARG
 #endif
 
 struct __attribute__((aligned(16))) V6Shared {
@@ -67,6 +76,12 @@ struct __attribute__((aligned(16))) V6Shared {
     int barb;
 };
 static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave buffer");
+
+// twiddle table (double2): [0, 4) forward pass A (uniform), [4, 260) forward pass B [4][64],
+// [260, 516) forward pass C, [516, 772) inverse pass B [4][64], [772, 1028) inverse pass A,
+// [1028, 1540) post-twist zeta^-(L + 64 r) [8][64]
+constexpr int kTwInv = 516;
+constexpr int kTwPost = 1028;
 
 struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
@@ -96,21 +111,6 @@ __device__ __forceinline__ void bf_fwd(Cx &u, Cx &v, const Cx &w) {
     u.im = xi;
 }
 
-// inverse of bf_fwd up to a factor 2: (u, v) -> (u + v, (u - v) conj(W)); 8 fp64 ops
-template <bool ODD>
-__device__ __forceinline__ void bf_inv(Cx &u, Cx &v, const Cx &w) {
-    const double dr = u.re - v.re, di = u.im - v.im;
-    u.re += v.re;
-    u.im += v.im;
-    if (!ODD) {   // d conj(w)
-        v.re = fma_(dr, w.re, di * w.im);
-        v.im = fma_(di, w.re, -(dr * w.im));
-    } else {      // d conj(i w) = -i d conj(w)
-        v.re = fma_(di, w.re, -(dr * w.im));
-        v.im = fma_(-dr, w.re, -(di * w.im));
-    }
-}
-
 // one radix-8 register pass: CT stages at register distance 4, 2, 1
 template <int NP>
 __device__ __forceinline__ void pass_fwd(Cx (&x)[NP][8], const Cx &w0, const Cx &w1, const Cx &w2a, const Cx &w2b) {
@@ -129,17 +129,56 @@ __device__ __forceinline__ void pass_fwd(Cx (&x)[NP][8], const Cx &w0, const Cx 
     }
 }
 
-__device__ __forceinline__ void pass_inv(Cx (&x)[8], const Cx &w0, const Cx &w1, const Cx &w2a, const Cx &w2b) {
-    bf_inv<false>(x[0], x[1], w2a);
-    bf_inv<true>(x[2], x[3], w2a);
-    bf_inv<false>(x[4], x[5], w2b);
-    bf_inv<true>(x[6], x[7], w2b);
-    bf_inv<false>(x[0], x[2], w1);
-    bf_inv<false>(x[1], x[3], w1);
-    bf_inv<true>(x[4], x[6], w1);
-    bf_inv<true>(x[5], x[7], w1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bf_inv<false>(x[r], x[r + 4], w0);
+// inverse: radix-2 DIT on the forward's bit-reversed output (slot n holds the evaluation at
+// zeta omega^brv9(n)), natural order out, then the zeta^-n post-twist (scripts/emu_v6.py
+// check_dit).  One register pass: stages at register distance 1, 2, 4 with per-lane twiddles
+// a, b (and -i b), c, c2 (and -i c, -i c2).
+__device__ __forceinline__ Cx negi_(const Cx &w) { return Cx{-w.re, -w.im}; }   // i (-w) = -i w
+__device__ __forceinline__ void pass_dit(Cx (&x)[8], const Cx &a, const Cx &b, const Cx &c, const Cx &c2) {
+    bf_fwd<false>(x[0], x[1], a);
+    bf_fwd<false>(x[2], x[3], a);
+    bf_fwd<false>(x[4], x[5], a);
+    bf_fwd<false>(x[6], x[7], a);
+    bf_fwd<false>(x[0], x[2], b);
+    bf_fwd<true>(x[1], x[3], negi_(b));
+    bf_fwd<false>(x[4], x[6], b);
+    bf_fwd<true>(x[5], x[7], negi_(b));
+    bf_fwd<false>(x[0], x[4], c);
+    bf_fwd<false>(x[1], x[5], c2);
+    bf_fwd<true>(x[2], x[6], negi_(c));
+    bf_fwd<true>(x[3], x[7], negi_(c2));
+}
+// W = 1 and W = -i butterflies: 4 adds
+__device__ __forceinline__ void bf_one(Cx &u, Cx &v) {
+    const Cx t = u;
+    u.re = t.re + v.re;
+    u.im = t.im + v.im;
+    v.re = t.re - v.re;
+    v.im = t.im - v.im;
+}
+__device__ __forceinline__ void bf_negi(Cx &u, Cx &v) {   // (u - i v, u + i v)
+    const Cx t = u;
+    u.re = t.re + v.im;
+    u.im = t.im - v.re;
+    const double vr = v.re;
+    v.re = t.re - v.im;
+    v.im = t.im + vr;
+}
+// pass C of the inverse: stages 0..2 (h = 1, 2, 4), twiddles 1, -i, e^{-i pi / 4}, -i e^{-i pi / 4}
+__device__ __forceinline__ void pass_dit_C(Cx (&x)[8]) {
+    constexpr double h = 0.70710678118654752440;
+    bf_one(x[0], x[1]);
+    bf_one(x[2], x[3]);
+    bf_one(x[4], x[5]);
+    bf_one(x[6], x[7]);
+    bf_one(x[0], x[2]);
+    bf_negi(x[1], x[3]);
+    bf_one(x[4], x[6]);
+    bf_negi(x[5], x[7]);
+    bf_one(x[0], x[4]);
+    bf_fwd<false>(x[1], x[5], Cx{h, -h});
+    bf_negi(x[2], x[6]);
+    bf_fwd<true>(x[3], x[7], Cx{-h, h});
 }
 
 __device__ __forceinline__ Cx ld(const double2 *p) {
@@ -154,6 +193,11 @@ struct Tw4 {
 };
 __device__ __forceinline__ Tw4 load_tw(const double2 *tw, int k, int L) {
     const double2 *t = tw + 4 + k * 256 + L;
+    return Tw4{ld(t), ld(t + 64), ld(t + 128), ld(t + 192)};
+}
+// inverse DIT twiddles of pass B (k = 0) or A (k = 1): a, b, c, c2
+__device__ __forceinline__ Tw4 load_tw_inv(const double2 *tw, int k, int L) {
+    const double2 *t = tw + kTwInv + k * 256 + L;
     return Tw4{ld(t), ld(t + 64), ld(t + 128), ld(t + 192)};
 }
 __device__ __forceinline__ Tw4 load_tw_uniform(const double2 *tw) {
@@ -319,8 +363,9 @@ struct RowTerms6 {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
+template <int WAVES>
 __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int L,
-                                        uint32_t (&acc)[16]) {
+                                        uint32_t (&acc)[16] V6_STAMPS_PARAM) {
     double2 *X = sh.X[w];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
@@ -355,12 +400,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC and the hand-over store.
     const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
-    Cx bv[2][8];
     const Tw4 tC = load_tw(g.tw, 1, L);
+    Cx Y[8];
+    Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     load_bk(bv, bk, 1 - w);
     __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
     fft_fwd_C<2>(D, tC);
-    Cx Y[8];
     mac6(D, bv, Y);
     V6_STAMP(2);
     load_bk(bv, bk, w);
@@ -379,23 +424,31 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
             Y[r].im += o[r].im;
         }
     }
-    {
-        const Tw4 t = load_tw(g.tw, 1, L);
-        pass_inv(Y, t.w0, t.w1, t.w2a, t.w2b);
-    }
-    const Tw4 tB = load_tw(g.tw, 0, L);
+    pass_dit_C(Y);
+    const Tw4 tB = load_tw_inv(g.tw, 0, L);
     V6_STAMP(5);
     lds_barrier6();   // the other wave has read X[w]
     V6_STAMP(6);
     store_C(X, Y, L);
     wave_sync();
     load_B_p(X, Y, L);
-    pass_inv(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
-    wave_sync();
-    store_B_ab(X, Y, L);
-    wave_sync();
-    load_A(X, Y, L);
-    pass_inv(Y, tA.w0, tA.w1, tA.w2a, tA.w2b);
+    pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
+    {
+        const Tw4 tI = load_tw_inv(g.tw, 1, L);
+        wave_sync();
+        store_B_ab(X, Y, L);
+        wave_sync();
+        load_A(X, Y, L);
+        pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
+    }
+    // post-twist zeta^-n, n = L + 64 r
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const Cx z = ld(g.tw + kTwPost + r * 64 + L);
+        const double re = fma_(Y[r].re, z.re, -(Y[r].im * z.im));
+        const double im = fma_(Y[r].re, z.im, Y[r].im * z.re);
+        Y[r] = Cx{re, im};
+    }
     V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im)
 #pragma unroll
@@ -407,6 +460,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     V6_STAMP(8);
 }
 
+template <int WAVES>
 __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub) {
     const int tid = threadIdx.x;
@@ -435,11 +489,19 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         for (int r = 0; r < 16; ++r)
             acc[r] = w == 0 ? 0u : (((L + 64 * r - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu);
     }
+#ifdef TFHE_AMD_V6_STAMPS
+    V6Stamps stamps;
+    stamps.prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = 0; i < kn; ++i) {
         const int a = sh.bara[i];
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6(sh, g, tA, i, a, w, L, acc);
+        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
     }
+#ifdef TFHE_AMD_V6_STAMPS
+    if (blockIdx.x == 0 && blockIdx.y == 0 && L == 0)
+        for (int k = 0; k < 10; ++k) g_v6_stamps[w][k] += stamps.acc[k];
+#endif
     // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
     if (w == 0) {
         uint32_t *E = reinterpret_cast<uint32_t *>(sh.X[0]);
@@ -455,7 +517,8 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     }
 }
 
-__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6(V6Args g, int B, BrInput in0, BrInput in1,
+template <int WAVES>
+__global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g, int B, BrInput in0, BrInput in1,
                                                                 int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
     __shared__ V6Shared sh;
@@ -468,10 +531,11 @@ __global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+    br_v6_body<WAVES>(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
 }
 
-__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, const CircRow *__restrict__ rows,
+template <int WAVES>
+__global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, const CircRow *__restrict__ rows,
                                                                      const int32_t *__restrict__ wa,
                                                                      const int32_t *__restrict__ wb, int32_t mu,
                                                                      int32_t *__restrict__ u_a,
@@ -491,10 +555,10 @@ __global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_
     wire(row.y, t.ya, t.yb);
     wire(row.z, t.za, t.zb);
     const size_t slot = (size_t)r * B + k;
-    br_v6_body(sh, g, t, mu, u_a + slot * kN, u_b + slot);
+    br_v6_body<WAVES>(sh, g, t, mu, u_a + slot * kN, u_b + slot);
 }
 
-__global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
+__global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
                                                                       const int32_t *__restrict__ bara) {
     __shared__ V6Shared sh;
     const int tid = threadIdx.x;
@@ -510,7 +574,10 @@ __global__ __launch_bounds__(kV6Threads, TFHE_AMD_V6_WAVES) void k_blind_rotate_
     for (int i = 0; i < iters; ++i) {
         const int a = sh.bara[i];
         if (a == 0) continue;
-        cmux_v6(sh, g, tA, i, a, w, L, ac);
+#ifdef TFHE_AMD_V6_STAMPS
+        V6Stamps stamps;
+#endif
+        cmux_v6<2>(sh, g, tA, i, a, w, L, ac V6_STAMPS_ARG);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];
@@ -558,6 +625,22 @@ void build_v6_twiddles(double2 *tw) {
     tw[1] = cis(W[1][0]);
     tw[2] = cis(W[2][0]);
     tw[3] = cis(W[2][2]);
+    auto cexp = [](long double num, long double den) {   // e^{-2 pi i num / den}
+        const long double th = -2.0L * 3.14159265358979323846264338327950288L * num / den;
+        return make_double2((double)cosl(th), (double)sinl(th));
+    };
+    for (int L = 0; L < 64; ++L) {
+        const int l7 = L & 7;
+        tw[kTwInv + 0 * 64 + L] = cexp(l7, 16);
+        tw[kTwInv + 1 * 64 + L] = cexp(l7, 32);
+        tw[kTwInv + 2 * 64 + L] = cexp(l7, 64);
+        tw[kTwInv + 3 * 64 + L] = cexp(8 * l7 + 64, 512);          // c e^{-i pi / 4}
+        tw[kTwInv + 256 + 0 * 64 + L] = cexp(L, 128);
+        tw[kTwInv + 256 + 1 * 64 + L] = cexp(L, 256);
+        tw[kTwInv + 256 + 2 * 64 + L] = cexp(L, 512);
+        tw[kTwInv + 256 + 3 * 64 + L] = cexp(L + 64, 512);
+        for (int r = 0; r < 8; ++r) tw[kTwPost + r * 64 + L] = cexp(L + 64 * r, 2048);   // zeta^-n
+    }
     for (int L = 0; L < 64; ++L) {
         const int g = L >> 3;
         tw[4 + 0 * 64 + L] = cis(W[3][g]);
@@ -588,8 +671,8 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     if (B <= 0) return hipSuccess;
     if (!key.bk_fft) return hipErrorInvalidValue;
     const BrInput in1 = halves > 1 ? in[1] : in[0];
-    hipLaunchKernelGGL(k_blind_rotate_v6, dim3(B * halves), dim3(kV6Threads), 0, s, v6_args(key), B, in[0], in1, mu,
-                       u_a, u_b);
+    hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3(B * halves), dim3(kV6Threads), 0, s, v6_args(key), B, in[0],
+                       in1, mu, u_a, u_b);
     return hipGetLastError();
 }
 
@@ -597,8 +680,8 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
     if (B <= 0 || nrows <= 0) return hipSuccess;
     if (nrows > 65535 || !key.bk_fft) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_v6_rows, dim3(B, nrows), dim3(kV6Threads), 0, s, v6_args(key), B, rows, wa, wb,
-                       mu, u_a, u_b);
+    hipLaunchKernelGGL(k_blind_rotate_v6_rows<kV6Waves>, dim3(B, nrows), dim3(kV6Threads), 0, s, v6_args(key), B, rows,
+                       wa, wb, mu, u_a, u_b);
     return hipGetLastError();
 }
 

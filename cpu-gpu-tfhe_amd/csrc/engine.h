@@ -15,7 +15,7 @@ struct DeviceKey {
     uint2 *tw2 = nullptr;         // v2 twiddles: uniform fwd/inv [2][16] x2, streams [2][27][64], [2][18][64]
     uint2 *tw4 = nullptr;         // v4 inverse-CT twiddles: uniform [2][16], streams [2][27][64], post-twist [2][16][64]
     double2 *bk_fft = nullptr;    // v6: [kn][4 rows][2 c][8 r][64 L] FFT-domain key / 512 (slot 8 L + r)
-    double2 *tw6 = nullptr;       // v6 twiddles: [4] uniform + [4][64] pass B + [4][64] pass C
+    double2 *tw6 = nullptr;       // v6 twiddles: forward [4] + [4][64] x 2, inverse [4][64] x 2, post-twist [8][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     int32_t *ksk4 = nullptr;      // ks-v4: [126 column blocks][kN][kKsT][3][4]
     NttTables *tables = nullptr;  // device copy
@@ -25,7 +25,7 @@ struct DeviceKey {
 };
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
-constexpr int kTw6Words = 4 + 2 * 4 * 64;   // double2 entries
+constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64;   // double2 entries (blind_rotate_v6.hip)
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
