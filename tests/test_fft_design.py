@@ -1,0 +1,53 @@
+"""The v6 blind rotation's fp64 FFT external product, checked on the CPU through
+scripts/emu_v6.py — a numpy emulation of the kernel's exact data flow: twiddle tree, the three
+radix-8 register passes and their layouts, the DIT inverse on the bit-reversed output and the
+post-twist.  The GPU kernel itself is compared with the exact-NTT kernels and the oracle in
+tests/test_gpu_parity.py (-m gpu)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+import emu_v6 as E  # noqa: E402
+
+
+def test_twiddle_tree_roots_and_order():
+    W, roots = E.twiddles_v6()
+    # stage s has 2^s blocks; odd blocks are i x their even sibling (only even ones stored)
+    for s, ws in enumerate(W):
+        assert len(ws) == 2 ** s
+        for b in range(1, len(ws), 2):
+            assert (ws[b] - ws[b - 1]) % E.M == 2048
+    # forward slot n evaluates at zeta omega^brv9(n): the DIT inverse relies on this order
+    brv = [int(format(n, "09b")[::-1], 2) for n in range(512)]
+    assert roots == [(16 * brv[n] + 4) % E.M for n in range(512)]
+
+
+def _exact(d, bk):
+    return sum(E.negacyclic(d[p], bk[p]) for p in range(len(d)))
+
+
+def test_external_product_exact_with_margin(rng):
+    T = E.tables()
+    d = rng.integers(-512, 512, (4, 1024))
+    bk = rng.integers(-2**31, 2**31, (4, 1024))
+    acc = sum(E.fwd(d[p].astype(float), T) * (E.fwd(bk[p].astype(float), T) / 512) for p in range(4))
+    want = _exact(d, bk)
+    for inv in (E.inv, E.inv_dit):
+        c = inv(acc) if inv is E.inv_dit else inv(acc, T)
+        assert all(int(g) == int(w) for g, w in zip(np.rint(c).astype(np.int64), want))
+        assert np.max(np.abs(c - np.rint(c))) < 0.125          # rounding margin (1/2 needed)
+
+
+def test_saturated_digits_stay_exact():
+    """Extreme but valid inputs: every digit -512 against random keys (the largest |c| the
+    decomposition can produce for a given key), and alternating extremes."""
+    T = E.tables()
+    r = np.random.default_rng(11)
+    bk = r.integers(-2**31, 2**31, (4, 1024))
+    for d in (np.full((4, 1024), -512), np.where(np.arange(1024) % 2 == 0, 511, -512)[None, :].repeat(4, 0)):
+        acc = sum(E.fwd(d[p].astype(float), T) * (E.fwd(bk[p].astype(float), T) / 512) for p in range(4))
+        c = E.inv_dit(acc)
+        want = _exact(d, bk)
+        assert all(int(g) == int(w) for g, w in zip(np.rint(c).astype(np.int64), want))
