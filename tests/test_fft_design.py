@@ -51,3 +51,23 @@ def test_saturated_digits_stay_exact():
         c = E.inv_dit(acc)
         want = _exact(d, bk)
         assert all(int(g) == int(w) for g, w in zip(np.rint(c).astype(np.int64), want))
+
+
+def test_p3_distance_to_truncating_fft(rng):
+    """SURVEY.md §8(c) P3 (diagnostic): the reference's FFTW path converts back with
+    Torus32(int64_t(x / N * 2^32)) (fft_processor_fftw.cu:177), i.e. it TRUNCATES the double
+    result instead of rounding it.  Emulated on the same transform, that mode differs from the
+    exact product (which the engine returns, P1) by exactly 1 on about half of the
+    coefficients and never by more."""
+    T = E.tables()
+    d = rng.integers(-512, 512, (4, 1024))
+    bk = rng.integers(-2**31, 2**31, (4, 1024))
+    acc = sum(E.fwd(d[p].astype(float), T) * (E.fwd(bk[p].astype(float), T) / 512) for p in range(4))
+    c = E.inv_dit(acc)
+    exact = np.array([int(x) for x in _exact(d, bk)], dtype=np.int64)
+    trunc = np.trunc(c).astype(np.int64)
+    delta = np.abs(trunc - exact)
+    frac = float(np.mean(delta != 0))
+    print(f"P3: truncating-FFT mode differs from the exact product on {frac:.1%} of coefficients "
+          f"(max |delta| = {int(delta.max())})")
+    assert delta.max() <= 1 and 0.3 < frac < 0.7
