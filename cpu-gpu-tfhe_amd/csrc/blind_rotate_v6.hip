@@ -25,7 +25,10 @@
 //  * each wave has ONE 9 KB LDS buffer: per step it holds the periodic negacyclic extension
 //    E[k] = +-acc[k mod N] (k < 2240: the rotation X^a reads E[(j - a) mod 2N] with one base per
 //    quarter of the lane's coefficients), then the FFT transposes, then the partial sum handed
-//    to the other wave (19.5 KB per ciphertext).
+//    to the other wave; the per-lane twiddles are read from a 17 KB LDS copy (36.5 KB per
+//    ciphertext, 4 workgroups per CU), so the key is the only global load in the loop.
+//  * issue priority is steered per launch (set_prio_level): by step for multi-round launches,
+//    rotating for single-round ones.
 #include <cmath>
 #include <vector>
 #include "engine.h"
@@ -57,6 +60,20 @@ struct V6Stamps {
         stamps.acc[k] += now - stamps.prev;                          \
         stamps.prev = now;                                           \
     } while (0)
+// per-workgroup wall-clock window and placement: [start_rt, end_rt, start_clk, end_clk, hw_id, xcc_id]
+// (s_memrealtime: constant 100 MHz; s_memtime: shader clock), read with tfhe_amd_debug_v6_wgtime
+constexpr int kWgSlots = 8192;
+__device__ unsigned long long g_v6_wg[kWgSlots][6];
+__device__ __forceinline__ unsigned int hwreg_hw_id() {
+    unsigned int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+__device__ __forceinline__ unsigned int hwreg_xcc_id() {
+    unsigned int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v;
+}
 #define V6_STAMPS_PARAM , V6Stamps &stamps
 #define V6_STAMPS_ARG , stamps
 #else
@@ -69,13 +86,31 @@ struct __attribute__((aligned(16))) V6Shared {
     double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
+    double2 tw[kT7Words];            // per-lane twiddles (compact table, fft_wave.h)
 };
 static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave buffer");
 
 struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
-    const double2 *tw;   // [4] uniform (pass A) + [4][64] (pass B) + [4][64] (pass C)
+    const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
+    int prio;            // issue-priority policy, see set_prio_level
 };
+
+// Issue priority.  A SIMD's two waves (different workgroups) are arbitrated by priority, then
+// age, so by default the oldest workgroup of a CU runs ahead and the youngest trails (B = 1024:
+// 2.7 ms vs 3.9 ms per workgroup, scripts/v6_wgtime.py).  Policy 1 (launches with more
+// workgroups than fit at once): priority 3 - i / 128 by step, so workgroups dispatched later,
+// still early in their 500 steps, go first (B = 4096: -11 %).  Policy 2 (one round of
+// workgroups): every 8 steps each workgroup moves to the next of the 4 levels from a hashed
+// offset, so all share the SIMDs evenly (B = 1024: -4 %).  Policy 0: hardware default.
+__device__ __forceinline__ void set_prio_level(unsigned lvl) {
+    switch (lvl & 3) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
 
 
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
@@ -112,13 +147,13 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     }
     wave_sync();
     V6_STAMP(0);
-    fft_fwd_AB<2>(D, X, g.tw, tA, L);
+    fft_fwd_AB_t<2>(D, X, tA, tw7_fwdB(sh.tw, L), L);
     V6_STAMP(1);
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC and the hand-over store.
     const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
-    const Tw4 tC = load_tw(g.tw, 1, L);
+    const Tw4 tC = tw7_fwdC(sh.tw, L);
     Cx Y[8];
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     load_bk(bv, bk, 1 - w);
@@ -143,7 +178,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
         }
     }
     pass_dit_C(Y);
-    const Tw4 tB = load_tw_inv(g.tw, 0, L);
+    const Tw4 tB = tw7_invB(sh.tw, L);
     V6_STAMP(5);
     lds_barrier6();   // the other wave has read X[w]
     V6_STAMP(6);
@@ -152,7 +187,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     load_B_p(X, Y, L);
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
-        const Tw4 tI = load_tw_inv(g.tw, 1, L);
+        const Tw4 tI = tw7_invA(sh.tw, L);
         wave_sync();
         store_B_ab(X, Y, L);
         wave_sync();
@@ -162,7 +197,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     // post-twist zeta^-n, n = L + 64 r
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        const Cx z = ld(g.tw + kTwPost + r * 64 + L);
+        const Cx z = ld(sh.tw + kT7Post + r * 64 + L);
         const double re = fma_(Y[r].re, z.re, -(Y[r].im * z.im));
         const double im = fma_(Y[r].re, z.im, Y[r].im * z.re);
         Y[r] = Cx{re, im};
@@ -184,6 +219,15 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
+#ifdef TFHE_AMD_V6_STAMPS
+    const int wg = blockIdx.x + blockIdx.y * gridDim.x;
+    if (tid == 0 && wg < kWgSlots) {
+        g_v6_wg[wg][0] = __builtin_amdgcn_s_memrealtime();
+        g_v6_wg[wg][2] = __builtin_amdgcn_s_memtime();
+        g_v6_wg[wg][4] = hwreg_hw_id();
+        g_v6_wg[wg][5] = hwreg_xcc_id();
+    }
+#endif
     // gate prologue + modulus switching (lwe-bootstrapping-functions-fft.cu:1851-1858)
     for (int i = tid; i < kn; i += kV6Threads) {
         uint32_t x = t.xa ? (uint32_t)t.sa * (uint32_t)t.xa[i] : 0u;
@@ -197,6 +241,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
+    for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
@@ -211,7 +256,13 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     V6Stamps stamps;
     stamps.prev = __builtin_amdgcn_s_memtime();
 #endif
+    const int prio = g.prio;
     for (int i = 0; i < kn; ++i) {
+        if (prio == 1) {
+            if ((i & 127) == 0) set_prio_level(3 - (i >> 7));
+        } else if (prio == 2) {
+            if ((i & 7) == 0) set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> 3));
+        }
         const int a = sh.bara[i];
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
         cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
@@ -233,6 +284,12 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     } else if (L == 0) {
         *ub = (int32_t)acc[0];
     }
+#ifdef TFHE_AMD_V6_STAMPS
+    if (tid == 0 && wg < kWgSlots) {
+        g_v6_wg[wg][1] = __builtin_amdgcn_s_memrealtime();
+        g_v6_wg[wg][3] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 }
 
 template <int WAVES>
@@ -287,6 +344,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #pragma unroll
     for (int r = 0; r < 16; ++r) ac[r] = (uint32_t)accg[L + 64 * r];
     for (int i = tid; i < iters; i += kV6Threads) sh.bara[i] = (short)(bara[(size_t)blockIdx.x * iters + i] & (k2N - 1));
+    for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     for (int i = 0; i < iters; ++i) {
@@ -377,10 +435,23 @@ hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const doub
     return hipGetLastError();
 }
 
-static V6Args v6_args(const DeviceKey &key) {
+// priority policy for a launch of `wgs` 2-wave workgroups: 4 fit a CU (VGPRs)
+static int v6_prio_policy(const DeviceKey &key, long wgs) {
+    static int cus[64] = {0};
+    const int d = key.device >= 0 && key.device < 64 ? key.device : 0;
+    if (!cus[d]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, key.device) != hipSuccess || n <= 0) n = 256;
+        cus[d] = n;
+    }
+    return wgs > 4L * cus[d] ? 1 : 2;
+}
+
+static V6Args v6_args(const DeviceKey &key, long wgs) {
     V6Args g;
     g.bk = key.bk_fft;
     g.tw = key.tw6;
+    g.prio = wgs > 0 ? v6_prio_policy(key, wgs) : 0;
     return g;
 }
 
@@ -389,7 +460,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     if (B <= 0) return hipSuccess;
     if (!key.bk_fft) return hipErrorInvalidValue;
     const BrInput in1 = halves > 1 ? in[1] : in[0];
-    hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3(B * halves), dim3(kV6Threads), 0, s, v6_args(key), B, in[0],
+    hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3(B * halves), dim3(kV6Threads), 0, s, v6_args(key, (long)B * halves), B, in[0],
                        in1, mu, u_a, u_b);
     return hipGetLastError();
 }
@@ -398,7 +469,7 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
     if (B <= 0 || nrows <= 0) return hipSuccess;
     if (nrows > 65535 || !key.bk_fft) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_v6_rows<kV6Waves>, dim3(B, nrows), dim3(kV6Threads), 0, s, v6_args(key), B, rows,
+    hipLaunchKernelGGL(k_blind_rotate_v6_rows<kV6Waves>, dim3(B, nrows), dim3(kV6Threads), 0, s, v6_args(key, (long)B * nrows), B, rows,
                        wa, wb, mu, u_a, u_b);
     return hipGetLastError();
 }
@@ -407,7 +478,7 @@ hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, 
                                         hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (iters < 0 || iters > kn || !key.bk_fft) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_v6_debug, dim3(B), dim3(kV6Threads), 0, s, v6_args(key), iters, acc, bara);
+    hipLaunchKernelGGL(k_blind_rotate_v6_debug, dim3(B), dim3(kV6Threads), 0, s, v6_args(key, 0), iters, acc, bara);
     return hipGetLastError();
 }
 
@@ -423,5 +494,12 @@ extern "C" int tfhe_amd_debug_v6_stamps(unsigned long long *out, int reset) {
         (void)hipMemcpyToSymbol(HIP_SYMBOL(tfhe_amd::g_v6_stamps), z, sizeof z);
     }
     return 0;
+}
+extern "C" int tfhe_amd_debug_v6_wgtime(unsigned long long *out, int n) {
+    if (n > tfhe_amd::kWgSlots) n = tfhe_amd::kWgSlots;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tfhe_amd::g_v6_wg), (size_t)n * 6 * sizeof(unsigned long long)) ==
+                   hipSuccess
+               ? 0
+               : -2;
 }
 #endif

@@ -75,7 +75,7 @@ int br_version() {
     if (v < 0) {
         const char *e = getenv("TFHE_AMD_BR");
         v = e ? atoi(e) : 0;
-        if (v < 0 || v > 6) v = 0;
+        if (v < 0 || v > 7) v = 0;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
@@ -90,6 +90,7 @@ static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput 
     case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
     case 6: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
+    case 7: return launch_blind_rotate_v7(key, B, halves, in, mu, u_a, u_b, s);
     default: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
     }
 }
@@ -99,6 +100,7 @@ hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, cons
     switch (br_version()) {
     case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+    case 7: return launch_blind_rotate_v7_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     default: return launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     }
 }
@@ -464,6 +466,7 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
            : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
            : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
            : (v == 4 || v == 5) ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)   // v5 shares v4's math
+           : v == 7 ? launch_blind_rotate_v7_debug(c->key, B, iters, acc, bara, s)
                     : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
@@ -582,20 +585,20 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version < 0 || br_version > 6) return TFHE_AMD_E_ARG;
+    if (br_version < 0 || br_version > 7) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }
 
 extern "C" const char *tfhe_amd_version(void) {
     // one immutable string per (blind-rotation, key-switch) generation pair
-    static char names[7][5][48];
+    static char names[8][5][48];
     static std::once_flag once;
     std::call_once(once, [] {
-        for (int b = 0; b <= 6; b++)
+        for (int b = 0; b <= 7; b++)
             for (int k = 1; k <= 4; k++) {
-                if (b == 0 || b == 6)
-                    snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v6 ks-v%d", k);
+                if (b == 0 || b >= 6)
+                    snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v%d ks-v%d", b == 7 ? 7 : 6, k);
                 else snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
             }
     });

@@ -93,7 +93,15 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
 hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
-// which blind-rotation kernel runs: 0 = default (v6), 1..6 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
+// v7 (v6 arithmetic; BK_i staged in LDS by LDS-DMA and shared by the workgroup's ciphertexts),
+// blind_rotate_v7.hip; same results as v6
+hipError_t launch_blind_rotate_v7(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v7_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+hipError_t launch_blind_rotate_v7_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
+                                        const int32_t *bara, hipStream_t s);
+// which blind-rotation kernel runs: 0 = default (v6), 1..7 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
 // circuit level blind rotation with the selected kernel (rows variants of v4 / v5 / v6)
 hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,

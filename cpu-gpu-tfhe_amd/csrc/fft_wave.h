@@ -234,6 +234,26 @@ __device__ __forceinline__ void fft_fwd_AB(Cx (&x)[NP][8], double2 *X, const dou
         wave_sync();
     }
 }
+// the same with the pass-B twiddles supplied by the caller (v7: read from LDS)
+template <int NP>
+__device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const Tw4 &tA, const Tw4 &t, int L) {
+    pass_fwd<NP>(x, tA.w0, tA.w1, tA.w2a, tA.w2b);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_A(X, x[p], L);
+        wave_sync();
+        load_B_ab(X, x[p], L);
+        wave_sync();
+    }
+    pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        store_B_p(X, x[p], L);
+        wave_sync();
+        load_C(X, x[p], L);
+        wave_sync();
+    }
+}
 template <int NP>
 __device__ __forceinline__ void fft_fwd_C(Cx (&x)[NP][8], const Tw4 &tC) {
     pass_fwd<NP>(x, tC.w0, tC.w1, tC.w2a, tC.w2b);
@@ -265,6 +285,16 @@ __device__ __forceinline__ void write_ext(uint32_t *E, const uint32_t (&acc)[16]
 
 // BK_i rows 2w, 2w + 1 of output c for this lane: 16 x 16 B, all in flight together
 __device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c) {
+#ifdef TFHE_AMD_DIAG_NOBK
+    // timing diagnostic only (wrong results): no key traffic
+    const double s = 1e-9 * (double)(int)(reinterpret_cast<uintptr_t>(bk) & 0xffff);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        b[0][r] = Cx{s + r, s - c};
+        b[1][r] = Cx{s - r, s + c};
+    }
+    return;
+#endif
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         b[0][r] = ld(bk + c * 512 + r * 64);
@@ -288,6 +318,36 @@ __device__ __forceinline__ void mac6(const Cx (&D)[2][8], const Cx (&b)[2][8], C
     }
 }
 
+
+// compact LDS twiddle table (double2 entries): forward pass B [4][8] (by L >> 3), forward pass C
+// [4][64], inverse pass B [4][8] (by L & 7), inverse pass A [4][64], post-twist [8][64]
+constexpr int kT7FwdB = 0, kT7FwdC = 32, kT7InvB = 288, kT7InvA = 320, kT7Post = 576, kT7Words = 1088;
+
+// source index in the global v6 table (build_v6_twiddles) of compact entry e
+__device__ __forceinline__ int t7_src(int e) {
+    if (e < kT7FwdC) return 4 + (e >> 3) * 64 + (e & 7) * 8;
+    if (e < kT7InvB) return 260 + (e - kT7FwdC);
+    if (e < kT7InvA) return kTwInv + ((e - kT7InvB) >> 3) * 64 + ((e - kT7InvB) & 7);
+    if (e < kT7Post) return kTwInv + 256 + (e - kT7InvA);
+    return kTwPost + (e - kT7Post);
+}
+
+__device__ __forceinline__ Tw4 tw7_fwdB(const double2 *t, int L) {
+    const double2 *p = t + kT7FwdB + (L >> 3);
+    return Tw4{ld(p), ld(p + 8), ld(p + 16), ld(p + 24)};
+}
+__device__ __forceinline__ Tw4 tw7_fwdC(const double2 *t, int L) {
+    const double2 *p = t + kT7FwdC + L;
+    return Tw4{ld(p), ld(p + 64), ld(p + 128), ld(p + 192)};
+}
+__device__ __forceinline__ Tw4 tw7_invB(const double2 *t, int L) {
+    const double2 *p = t + kT7InvB + (L & 7);
+    return Tw4{ld(p), ld(p + 8), ld(p + 16), ld(p + 24)};
+}
+__device__ __forceinline__ Tw4 tw7_invA(const double2 *t, int L) {
+    const double2 *p = t + kT7InvA + L;
+    return Tw4{ld(p), ld(p + 64), ld(p + 128), ld(p + 192)};
+}
 
 // The linear combination x = (0, c) + sa X + sb Y + sc Z that feeds one blind rotation (gate
 // prologues boot-gates.cu:98-448; a circuit row adds a third input for MAJ / XOR3); y / z may

@@ -101,7 +101,7 @@ def version():
 
 
 def select_kernel(generation):
-    """tfhe_amd_select_kernel: blind-rotation kernel generation 1..4 (A/B and cross-checks)."""
+    """tfhe_amd_select_kernel: blind-rotation kernel generation 1..7 (A/B and cross-checks; 0 = default)."""
     _check(lib.tfhe_amd_select_kernel(int(generation)), "select_kernel")
 
 

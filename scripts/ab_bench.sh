@@ -1,9 +1,24 @@
 #!/usr/bin/env bash
 # A/B of library variants in one GPU session: scripts/ab_bench.sh name1 name2 ... ("base" = lib/)
+# (AB_BATCH, AB_REPS).  One summary line per run in gpurun_out/ab_summary.txt.
 set -u
+mkdir -p gpurun_out
+for rep in $(seq 1 ${AB_REPS:-1}); do
 for n in "$@"; do
-  if [ "$n" = base ]; then lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so; else lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so; fi
-  TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps 3 --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline > gpurun_out/ab_${n}_${AB_BATCH:-1024}.log 2>&1
-  rc=$?; echo "$n rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  # "base" = lib/ (default kernel), "brN" = lib/ with TFHE_AMD_BR=N, else variants/<name>/
+  br=0
+  case "$n" in
+    base) lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so ;;
+    br*) lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so; br=${n#br} ;;
+    *) lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so ;;
+  esac
+  log=gpurun_out/ab_${n}_${AB_BATCH:-1024}_$rep.log
+  TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline > $log 2>&1
+  rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; tail -5 $log; exit $rc; }
+  python3 -c "
+import json,sys
+d=[json.loads(l) for l in open('$log') if l.startswith('{')][-1]
+print('%-10s B=%-5s rep %s  %9.0f /s  br %.3f ms  ks %.3f ms  ok=%s' % ('$n', '${AB_BATCH:-1024}', $rep, d['value'], d['roofline']['kernel_ms'], d['roofline']['keyswitch_ms'], d['truth_table_ok']))" | tee -a gpurun_out/ab_summary.txt
+done
 done
 exit 0

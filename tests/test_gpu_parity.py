@@ -121,9 +121,9 @@ def test_device_batch_1024_truth_and_sampled_parity(ctx, okey, keyset, rng):
 
 
 def test_kernel_generations_agree(ctx, keyset, rng):
-    """Every blind-rotation generation (v1 LDS radix-2, v2, v3, v4, v5 exact NTT; v6 fp64 FFT,
-    whose rounded products equal the exact ones) gives identical Torus32 results on the same
-    gates and on explicit CMux steps."""
+    """Every blind-rotation generation (v1 LDS radix-2, v2, v3, v4, v5 exact NTT; v6, v7 fp64
+    FFT, whose rounded products equal the exact ones) gives identical Torus32 results on the
+    same gates and on explicit CMux steps."""
     torch = _torch()
     B, iters = 8, 6
     x = rng.integers(0, 2, B)
@@ -135,7 +135,7 @@ def test_kernel_generations_agree(ctx, keyset, rng):
     default = T.version()
     outs = {}
     try:
-        for v in (1, 2, 3, 4, 5, 6):
+        for v in (1, 2, 3, 4, 5, 6, 7):
             T.select_kernel(v)
             d_acc = torch.from_numpy(acc0.copy()).cuda()
             ctx.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), iters)
@@ -144,7 +144,7 @@ def test_kernel_generations_agree(ctx, keyset, rng):
     finally:
         tag = default.split("br-v")[1].split(" ")[0]
         T.select_kernel(int(tag) if tag.isdigit() else 0)
-    for v in (1, 2, 3, 5, 6):
+    for v in (1, 2, 3, 5, 6, 7):
         (ra, rb), acc = outs[v]
         (ra4, rb4), acc4 = outs[4]
         assert np.array_equal(ra, ra4) and np.array_equal(rb, rb4), v
