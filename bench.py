@@ -47,8 +47,8 @@ FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP), AMD spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -30,6 +30,7 @@
 //  * issue priority is steered per launch (set_prio_level): by step for multi-round launches,
 //    rotating for single-round ones.
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 #include "engine.h"
 #include "modarith.h"
@@ -94,6 +95,7 @@ struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
     const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
     int prio;            // issue-priority policy, see set_prio_level
+    int prio_shift;      // policy 2: steps per level = 2^prio_shift
 };
 
 // Issue priority.  A SIMD's two waves (different workgroups) are arbitrated by priority, then
@@ -188,10 +190,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
         const Tw4 tI = tw7_invA(sh.tw, L);
+#ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
         store_B_ab(X, Y, L);
         wave_sync();
         load_A(X, Y, L);
+#endif
         pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
     }
     // post-twist zeta^-n, n = L + 64 r
@@ -261,7 +265,8 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         if (prio == 1) {
             if ((i & 127) == 0) set_prio_level(3 - (i >> 7));
         } else if (prio == 2) {
-            if ((i & 7) == 0) set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> 3));
+            if ((i & ((1 << g.prio_shift) - 1)) == 0)
+                set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> g.prio_shift));
         }
         const int a = sh.bara[i];
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
@@ -444,6 +449,8 @@ static int v6_prio_policy(const DeviceKey &key, long wgs) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, key.device) != hipSuccess || n <= 0) n = 256;
         cus[d] = n;
     }
+    static const char *env = getenv("TFHE_AMD_PRIO");   // experiments: force a policy
+    if (env) return atoi(env);
     return wgs > 4L * cus[d] ? 1 : 2;
 }
 
@@ -452,6 +459,8 @@ static V6Args v6_args(const DeviceKey &key, long wgs) {
     g.bk = key.bk_fft;
     g.tw = key.tw6;
     g.prio = wgs > 0 ? v6_prio_policy(key, wgs) : 0;
+    static const char *sh = getenv("TFHE_AMD_PRIO_S");
+    g.prio_shift = sh ? atoi(sh) : 3;
     return g;
 }
 

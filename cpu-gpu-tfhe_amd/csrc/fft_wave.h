@@ -238,6 +238,7 @@ __device__ __forceinline__ void fft_fwd_AB(Cx (&x)[NP][8], double2 *X, const dou
 template <int NP>
 __device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const Tw4 &tA, const Tw4 &t, int L) {
     pass_fwd<NP>(x, tA.w0, tA.w1, tA.w2a, tA.w2b);
+#ifndef TFHE_AMD_DIAG_NOTRAB
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         store_A(X, x[p], L);
@@ -245,6 +246,7 @@ __device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const T
         load_B_ab(X, x[p], L);
         wave_sync();
     }
+#endif
     pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
