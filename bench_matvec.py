@@ -3,7 +3,7 @@ rows sharded over GPUs (cpu-gpu-tfhe_amd/matvec.py).  One process per GPU:
 
     python bench_matvec.py                                   # 1 GPU, all 64 rows
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench_matvec.py
-    python bench_matvec.py --rows-of 8 --world-of 8          # rehearse one rank's 1/8 shard
+    python bench_matvec.py --rank-of 0 --world-of 8          # rehearse one rank's 1/8 shard
 
 Timed region: every rank's whole circuit (all levels), bracketed by barrier + synchronize,
 max over ranks.  Each rank decrypts its rows and checks them against integer arithmetic
