@@ -83,6 +83,13 @@ __device__ __forceinline__ unsigned int hwreg_xcc_id() {
 #define V6_STAMPS_ARG
 #endif
 
+// issue-order fence for the LDS read groups of the inverse (TFHE_AMD_V6_NOFENCE: compiler order)
+#ifdef TFHE_AMD_V6_NOFENCE
+#define SCHED_FENCE() do {} while (0)
+#else
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 struct __attribute__((aligned(16))) V6Shared {
     double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
@@ -170,9 +177,13 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     V6_STAMP(3);
     lds_barrier6();
     V6_STAMP(4);
+    // Inverse.  Every LDS read group is issued whole before the arithmetic that consumes it
+    // (sched_barrier): at 252 VGPRs the scheduler otherwise sinks each ds_read to its use and
+    // waits lgkmcnt(0) per pair, or per post-twist twiddle, i.e. one LDS round trip each.
     {
         Cx o[8];
         load_C(sh.X[1 - w], o, L);
+        SCHED_FENCE();
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             Y[r].re += o[r].re;
@@ -187,24 +198,27 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     store_C(X, Y, L);
     wave_sync();
     load_B_p(X, Y, L);
+    SCHED_FENCE();
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
         const Tw4 tI = tw7_invA(sh.tw, L);
+        Cx z[8];                                 // post-twist zeta^-n, n = L + 64 r
+#pragma unroll
+        for (int r = 0; r < 8; ++r) z[r] = ld(sh.tw + kT7Post + r * 64 + L);
 #ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
         store_B_ab(X, Y, L);
         wave_sync();
         load_A(X, Y, L);
+        SCHED_FENCE();
 #endif
         pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
-    }
-    // post-twist zeta^-n, n = L + 64 r
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const Cx z = ld(sh.tw + kT7Post + r * 64 + L);
-        const double re = fma_(Y[r].re, z.re, -(Y[r].im * z.im));
-        const double im = fma_(Y[r].re, z.im, Y[r].im * z.re);
-        Y[r] = Cx{re, im};
+        for (int r = 0; r < 8; ++r) {
+            const double re = fma_(Y[r].re, z[r].re, -(Y[r].im * z[r].im));
+            const double im = fma_(Y[r].re, z[r].im, Y[r].im * z[r].re);
+            Y[r] = Cx{re, im};
+        }
     }
     V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im)
@@ -261,14 +275,16 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     stamps.prev = __builtin_amdgcn_s_memtime();
 #endif
     const int prio = g.prio;
+    int a_next = sh.bara[0];
     for (int i = 0; i < kn; ++i) {
+        const int a = a_next;
+        a_next = sh.bara[i + 1 < kn ? i + 1 : i];   // a step ahead: no LDS round trip at the loop head
         if (prio == 1) {
             if ((i & 127) == 0) set_prio_level(3 - (i >> 7));
         } else if (prio == 2) {
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> g.prio_shift));
         }
-        const int a = sh.bara[i];
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
         cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
     }
