@@ -131,6 +131,8 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     double2 *X = sh.X[w];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
+    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
+    Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     write_ext(E, acc, L);
     wave_sync();
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
@@ -161,10 +163,10 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC and the hand-over store.
-    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
     const Tw4 tC = tw7_fwdC(sh.tw, L);
     Cx Y[8];
-    Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
+    // (issuing them at the top of the step instead, in flight for the whole forward transform,
+    // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
     load_bk(bv, bk, 1 - w);
     __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
     fft_fwd_C<2>(D, tC);

@@ -150,3 +150,37 @@ def test_kernel_generations_agree(ctx, keyset, rng):
         assert np.array_equal(ra, ra4) and np.array_equal(rb, rb4), v
         assert np.array_equal(acc, acc4), v
     assert np.array_equal(keyset.decrypt(*outs[4][0]), x ^ y)
+
+
+def test_chunk_boundaries_bit_exact(ctx, okey, keyset, rng):
+    """Launches larger than one round of workgroups (4 per CU: 1024 ciphertexts on 256 CUs) are
+    split into one-round launches; the ciphertexts on both sides of every split, and of the MUX
+    halves (2B rotations in one launch), match the oracle bit for bit."""
+    B = 1100
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - (x & y))
+    idx = np.array([0, 1, 1022, 1023, 1024, 1025, 1099])
+    o_a, o_b = okey.gate_batch("NAND", a_a[idx], a_b[idx], b_a[idx], b_b[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+    B = 600                                   # MUX: 1200 rotations, split at 1024 (inside half 1)
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    r_a, r_b = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), np.where(s == 1, x, y))
+    idx = np.array([0, 423, 424, 425, 599])   # half-1 rotation 424 is ciphertext 1024
+    o_a, o_b = okey.gate_batch("MUX", sa[idx], sb[idx], xa[idx], xb[idx], ya[idx], yb[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+
+
+def test_empty_batch_is_a_no_op(ctx, keyset, rng):
+    torch = _torch()
+    e2 = torch.empty((0, n), dtype=torch.int32, device="cuda")
+    e1 = torch.empty(0, dtype=torch.int32, device="cuda")
+    ctx.gate_dev("NAND", e2, e1, e2, e1, e2, e1)
+    ctx.sync()
+    x = rng.integers(0, 2, 3)
+    a_a, a_b = keyset.encrypt(x, rng)
+    r_a, r_b = ctx.gate_host("NOR", a_a, a_b, a_a, a_b)   # the context still works afterwards
+    assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - x)
