@@ -357,6 +357,49 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
     }
 }
 
+// ---------------------------------------------------------------- small batches
+// ks-v4 streams each 4-column slice of the key through one workgroup per 256 ciphertexts: for
+// a handful of ciphertexts that is 126 workgroups running a 32-chunk loop for one live lane
+// each (0.16 ms at B = 1).  For small batches the work is spread over key indices instead:
+// workgroup (chunk, ct) takes 16 key indices i of ciphertext ct, thread = output column
+// (row layout [i][j][h-1][512], column 500 = b), sums its 128 rows (a digit-0 row is loaded
+// and multiplied by 0 so that all loads are independent) and adds the partial into the
+// result with one 32-bit atomic add (wrapping, so the sum is the exact Torus32 value whatever
+// the order); the result rows are zeroed first (k_keyswitch_small_init), lane b gets u_b.
+constexpr int kKsSmallChunks = 64;
+constexpr int kKsSmallI = kN / kKsSmallChunks;   // 16 key indices per workgroup
+
+template <class P>
+__global__ __launch_bounds__(512) void k_keyswitch_small_init(P io) {
+    const KsLane ln = io.lane(blockIdx.x);
+    const int col = threadIdx.x;
+    if (col < kn) ln.ra[col] = 0;
+    else if (col == kn) *ln.rb = (int32_t)ln.b;
+}
+
+template <class P>
+__global__ __launch_bounds__(512) void k_keyswitch_small(const int32_t *__restrict__ ksk, P io) {
+    const int chunk = blockIdx.x, col = threadIdx.x;
+    const KsLane ln = io.lane(blockIdx.y);
+    if (col > kn) return;
+    const int i0 = chunk * kKsSmallI;
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (int ii = 0; ii < kKsSmallI; ++ii) {
+        const int i = i0 + ii;
+        const uint32_t ab = (uint32_t)ln.ua[i] + (ln.ua2 ? (uint32_t)ln.ua2[i] : 0u) + kKsPrecOffset;
+        const int32_t *row = ksk + (size_t)i * kKsT * 3 * kKsRow + col;
+#pragma unroll
+        for (int j = 0; j < kKsT; ++j) {
+            const uint32_t h = (ab >> (32 - (j + 1) * kKsBasebit)) & (kKsBase - 1);
+            const uint32_t v = (uint32_t)row[(j * 3 + (int)(h ? h : 1u) - 1) * kKsRow];
+            acc -= h ? v : 0u;
+        }
+    }
+    int32_t *dst = col < kn ? ln.ra + col : ln.rb;
+    atomicAdd(reinterpret_cast<unsigned int *>(dst), acc);
+}
+
 // packed KSK [i][j][h - 1][kKsRow] -> v4 [cb][i][j][h - 1][4 cols]
 __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ ksk, uint4 *__restrict__ ksk4) {
     const size_t pieces = (size_t)kKs4Blocks * kN * kKsT * 3;
@@ -369,11 +412,25 @@ __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ k
 
 }  // namespace
 
+// largest key-switch count that takes the small-batch kernels (TFHE_AMD_KS_SMALL overrides)
+static int ks_small_max() {
+    static const int v = [] {
+        const char *e = getenv("TFHE_AMD_KS_SMALL");
+        return e ? atoi(e) : 96;   // crossover with ks-v4 measured between 64 and 128
+    }();
+    return v;
+}
+
 hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const CircKs *ks, const int32_t *u_a,
                                  const int32_t *u_b, int32_t *wa, int32_t *wb, hipStream_t s) {
     if (B <= 0 || nks <= 0) return hipSuccess;
-    const int groups = (int)(((size_t)B * nks + kKs4Threads - 1) / kKs4Threads);
     KsRows io{ks, u_a, u_b, wa, wb, B, nks};
+    if ((long)B * nks <= ks_small_max()) {
+        hipLaunchKernelGGL(k_keyswitch_small_init<KsRows>, dim3(B * nks), dim3(512), 0, s, io);
+        hipLaunchKernelGGL(k_keyswitch_small<KsRows>, dim3(kKsSmallChunks, B * nks), dim3(512), 0, s, key.ksk, io);
+        return hipGetLastError();
+    }
+    const int groups = (int)(((size_t)B * nks + kKs4Threads - 1) / kKs4Threads);
     hipLaunchKernelGGL(k_keyswitch_v4<KsRows>, dim3(128 * groups), dim3(kKs4Threads), 0, s,
                        reinterpret_cast<const uint4 *>(key.ksk4), io);
     return hipGetLastError();
@@ -433,6 +490,10 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
         const int blocks = ((B + kKsCt - 1) / kKsCt) * 8;
         hipLaunchKernelGGL(k_keyswitch_v3, dim3(blocks), dim3(kKsV2Threads), 0, s, key.ksk, B, u_a, u_b, u2_a,
                            u2_b, add_b, res_a, res_b);
+    } else if (B <= ks_small_max()) {
+        KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
+        hipLaunchKernelGGL(k_keyswitch_small_init<KsPlain>, dim3(B), dim3(512), 0, s, io);
+        hipLaunchKernelGGL(k_keyswitch_small<KsPlain>, dim3(kKsSmallChunks, B), dim3(512), 0, s, key.ksk, io);
     } else {
         const int groups = (B + kKs4Threads - 1) / kKs4Threads;
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
