@@ -118,9 +118,11 @@ __device__ __forceinline__ void cmux_v7(V7Shared<C> &sh, const double2 *bk, cons
     mac6(D, bv, Y);
     barrier_lds();                                   // B2: partials stored, BK_i fully read
     if (i + 1 < iters) dma_key(sh, bk, i + 1, wv, L);
+    // inverse: LDS read groups issued whole before their arithmetic (as in v6)
     {
         Cx o[8];
         load_C(sh.X[wv ^ 1], o, L);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             Y[r].re += o[r].re;
@@ -133,21 +135,25 @@ __device__ __forceinline__ void cmux_v7(V7Shared<C> &sh, const double2 *bk, cons
     store_C(X, Y, L);
     wave_sync();
     load_B_p(X, Y, L);
+    __builtin_amdgcn_sched_barrier(0);
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
         const Tw4 tI = tw7_invA(sh.tw, L);
+        Cx z[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) z[r] = ld(sh.tw + kT7Post + r * 64 + L);
         wave_sync();
         store_B_ab(X, Y, L);
         wave_sync();
         load_A(X, Y, L);
+        __builtin_amdgcn_sched_barrier(0);
         pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
-    }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const Cx z = ld(sh.tw + kT7Post + r * 64 + L);
-        const double re = fma_(Y[r].re, z.re, -(Y[r].im * z.im));
-        const double im = fma_(Y[r].re, z.im, Y[r].im * z.re);
-        Y[r] = Cx{re, im};
+        for (int r = 0; r < 8; ++r) {
+            const double re = fma_(Y[r].re, z[r].re, -(Y[r].im * z[r].im));
+            const double im = fma_(Y[r].re, z[r].im, Y[r].im * z[r].re);
+            Y[r] = Cx{re, im};
+        }
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
