@@ -269,12 +269,17 @@ struct KsRows {                // circuit level: lane ct = g B + k -> wire ks[g]
     }
 };
 
-template <class P>
+// SPLIT > 1: the key indices are split over SPLIT workgroups per (column block, ciphertext
+// group), each adds its partial sums into result rows zeroed (and given b) by
+// k_keyswitch_small_init: more waves in flight for mid-size batches.
+template <class P, int SPLIT>
 __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__restrict__ ksk4, P io) {
     // buf[b][i][j][h][4 cols]: h = 0 is the zero row of lwe-keyswitch-functions.cu:919
     __shared__ __attribute__((aligned(16))) uint4 buf[2][kKs4I * kKsT * 4];   // 2 x 16 KB
+    const int part = SPLIT > 1 ? (int)(blockIdx.x % SPLIT) : 0;
+    const int bid = SPLIT > 1 ? (int)(blockIdx.x / SPLIT) : (int)blockIdx.x;
     // XCD-aware: workgroups with equal blockIdx % 8 stream the same column blocks
-    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int xcd = bid & 7, k = bid >> 3;
     const int cb = (k & 15) * 8 + xcd;
     const int ctg = k >> 4;
     if (cb >= kKs4Blocks) return;                 // whole workgroup: no barrier skipped
@@ -287,11 +292,13 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
     uint32_t acc[kKs4Cols];
 #pragma unroll
     for (int c = 0; c < kKs4Cols; ++c) acc[c] = 0;
-    if (cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols) acc[kn - cb * kKs4Cols] = ln.b;
+    if (SPLIT == 1 && cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols) acc[kn - cb * kKs4Cols] = ln.b;
+    constexpr int kIPart = kN / SPLIT;
+    const int ibeg = part * kIPart, iend = ibeg + kIPart;
 
-    const uint4 *src = ksk4 + (size_t)cb * kN * kKsT * 3 + tid;
-    const uint4 *pa = reinterpret_cast<const uint4 *>(ln.ua);
-    const uint4 *pa2 = reinterpret_cast<const uint4 *>(ln.ua2);
+    const uint4 *src = ksk4 + ((size_t)cb * kN + ibeg) * kKsT * 3 + tid;
+    const uint4 *pa = reinterpret_cast<const uint4 *>(ln.ua + ibeg);
+    const uint4 *pa2 = ln.ua2 ? reinterpret_cast<const uint4 *>(ln.ua2 + ibeg) : nullptr;
     // (i, j, h - 1) piece t = tid + 256 l of a chunk goes to buf[.][(t / 3) * 4 + t % 3 + 1]
     int dst[3];
 #pragma unroll
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
     }
     buf[0][dst[0]] = p0; buf[0][dst[1]] = p1; buf[0][dst[2]] = p2;
     __syncthreads();
-    for (int i0 = 0, b = 0; i0 < kN; i0 += kKs4I, b ^= 1) {
+    for (int i0 = 0, b = 0; i0 < kIPart; i0 += kKs4I, b ^= 1) {
         uint32_t a[kKs4I];
 #pragma unroll
         for (int v = 0; v < kKs4I / 4; ++v) {
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
             a[4 * v + 2] = av[v].z + av2[v].z + kKsPrecOffset;
             a[4 * v + 3] = av[v].w + av2[v].w + kKsPrecOffset;
         }
-        const bool more = i0 + kKs4I < kN;
+        const bool more = i0 + kKs4I < kIPart;
         if (more) {                                          // next chunk, in flight during the gather
             const uint4 *sn = src + (size_t)(i0 + kKs4I) * kKsT * 3;
             p0 = sn[0]; p1 = sn[kKs4Threads]; p2 = sn[2 * kKs4Threads];
@@ -352,8 +359,10 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
 #pragma unroll
     for (int c = 0; c < kKs4Cols; ++c) {
         const int col = cb * kKs4Cols + c;
-        if (col < kn) ln.ra[col] = (int32_t)acc[c];
-        else if (col == kn) *ln.rb = (int32_t)acc[c];
+        int32_t *dst = col < kn ? ln.ra + col : col == kn ? ln.rb : nullptr;
+        if (!dst) continue;
+        if (SPLIT > 1) atomicAdd(reinterpret_cast<unsigned int *>(dst), acc[c]);   // wrapping: exact
+        else *dst = (int32_t)acc[c];
     }
 }
 
@@ -412,6 +421,29 @@ __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ k
 
 }  // namespace
 
+// ks-v4 launch: batches of at most `ks_split_max()` key switches split the key indices over 2
+// workgroups (atomic partial sums into zeroed rows) so that more waves are in flight when the
+// batch gives fewer than 2 waves per SIMD (B = 128: 0.162 -> 0.093 ms, 256: 0.169 -> 0.102,
+// 512: 0.172 -> 0.129, 768: 0.217 -> 0.165)
+static int ks_split_max() {
+    static const int v = [] {
+        const char *e = getenv("TFHE_AMD_KS_SPLIT");
+        return e ? atoi(e) : 768;   // 128..768: -28..-43 %; 1024 / 4096: +1..3 % (measured)
+    }();
+    return v;
+}
+template <class P>
+static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io, hipStream_t s) {
+    if (count <= ks_split_max()) {
+        hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
+        hipLaunchKernelGGL((k_keyswitch_v4<P, 2>), dim3(2 * 128 * groups), dim3(kKs4Threads), 0, s,
+                           reinterpret_cast<const uint4 *>(key.ksk4), io);
+    } else {
+        hipLaunchKernelGGL((k_keyswitch_v4<P, 1>), dim3(128 * groups), dim3(kKs4Threads), 0, s,
+                           reinterpret_cast<const uint4 *>(key.ksk4), io);
+    }
+}
+
 // largest key-switch count that takes the small-batch kernels (TFHE_AMD_KS_SMALL overrides)
 static int ks_small_max() {
     static const int v = [] {
@@ -431,8 +463,7 @@ hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const Cir
         return hipGetLastError();
     }
     const int groups = (int)(((size_t)B * nks + kKs4Threads - 1) / kKs4Threads);
-    hipLaunchKernelGGL(k_keyswitch_v4<KsRows>, dim3(128 * groups), dim3(kKs4Threads), 0, s,
-                       reinterpret_cast<const uint4 *>(key.ksk4), io);
+    launch_ks4(key, groups, B * nks, io, s);
     return hipGetLastError();
 }
 
@@ -497,8 +528,7 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
     } else {
         const int groups = (B + kKs4Threads - 1) / kKs4Threads;
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
-        hipLaunchKernelGGL(k_keyswitch_v4<KsPlain>, dim3(128 * groups), dim3(kKs4Threads), 0, s,
-                           reinterpret_cast<const uint4 *>(key.ksk4), io);
+        launch_ks4(key, groups, B, io, s);
     }
     return hipGetLastError();
 }
