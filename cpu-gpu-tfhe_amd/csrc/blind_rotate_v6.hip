@@ -162,7 +162,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     V6_STAMP(1);
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
-    // flight during pass C, the second during the first MAC and the hand-over store.
+    // flight during pass C, the second during the first MAC, the hand-over and the barrier.
     const Tw4 tC = tw7_fwdC(sh.tw, L);
     Cx Y[8];
     // (issuing them at the top of the step instead, in flight for the whole forward transform,
@@ -175,7 +175,8 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     load_bk(bv, bk, w);
     __builtin_amdgcn_sched_barrier(0);
     store_C(X, Y, L);
-    mac6(D, bv, Y);
+    // the second MAC runs after the barrier and the partner-partial loads, so that its key
+    // loads land during those waits (B = 1: 1.69 -> 1.65 ms, B = 1024: -1 %)
     V6_STAMP(3);
     lds_barrier6();
     V6_STAMP(4);
@@ -186,6 +187,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
         Cx o[8];
         load_C(sh.X[1 - w], o, L);
         SCHED_FENCE();
+        mac6(D, bv, Y);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             Y[r].re += o[r].re;
