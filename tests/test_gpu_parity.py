@@ -184,3 +184,26 @@ def test_empty_batch_is_a_no_op(ctx, keyset, rng):
     a_a, a_b = keyset.encrypt(x, rng)
     r_a, r_b = ctx.gate_host("NOR", a_a, a_b, a_a, a_b)   # the context still works afterwards
     assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - x)
+
+
+@pytest.mark.parametrize("B", [1, 96, 97, 400, 768, 769])
+def test_keyswitch_paths_bit_exact(ctx, okey, rng, B):
+    """Each key-switch path (small batch <= 96 via per-key-index workgroups and atomic partials,
+    97..768 via the key-index split of ks-v4, > 768 plain ks-v4) at and around its threshold."""
+    u_a = rng.integers(-2**31, 2**31, (B, N), dtype=np.int64).astype(np.int32)
+    u_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    k_a, k_b = ctx.keyswitch_host(u_a, u_b)
+    o_a, o_b = okey.keyswitch_batch(u_a, u_b)
+    assert np.array_equal(k_a, o_a) and np.array_equal(k_b, o_b)
+
+
+def test_mux_split_keyswitch(ctx, okey, keyset, rng):
+    """MUX key-switches u1 + u2 + (0, 1/8): the two-input form through the split path."""
+    B = 300
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    r_a, r_b = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), np.where(s == 1, x, y))
+    idx = np.array([0, 150, 299])
+    o_a, o_b = okey.gate_batch("MUX", sa[idx], sb[idx], xa[idx], xb[idx], ya[idx], yb[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
