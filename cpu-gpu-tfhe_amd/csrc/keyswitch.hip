@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
     for (int c = 0; c < kKs4Cols; ++c) acc[c] = 0;
     if (SPLIT == 1 && cb * kKs4Cols <= kn && kn < cb * kKs4Cols + kKs4Cols) acc[kn - cb * kKs4Cols] = ln.b;
     constexpr int kIPart = kN / SPLIT;
-    const int ibeg = part * kIPart, iend = ibeg + kIPart;
+    const int ibeg = part * kIPart;
 
     const uint4 *src = ksk4 + ((size_t)cb * kN + ibeg) * kKsT * 3 + tid;
     const uint4 *pa = reinterpret_cast<const uint4 *>(ln.ua + ibeg);
