@@ -207,7 +207,7 @@ __device__ __forceinline__ void v7_modswitch(V7Shared<C> &sh, const RowTerms6 &t
 }
 
 template <int C>
-__global__ __launch_bounds__(128 * C, 2) void k_blind_rotate_v7(const double2 *__restrict__ bk,
+__global__ __launch_bounds__(128 * C, C == 4 ? 2 : 1) void k_blind_rotate_v7(const double2 *__restrict__ bk,
                                                                 const double2 *__restrict__ tw, int B, int nct,
                                                                 BrInput in0, BrInput in1, int32_t mu,
                                                                 int32_t *__restrict__ u_a, int32_t *__restrict__ u_b) {
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(128 * C, 2) void k_blind_rotate_v7(const double2 *_
 }
 
 template <int C>
-__global__ __launch_bounds__(128 * C, 2) void k_blind_rotate_v7_rows(const double2 *__restrict__ bk,
+__global__ __launch_bounds__(128 * C, C == 4 ? 2 : 1) void k_blind_rotate_v7_rows(const double2 *__restrict__ bk,
                                                                      const double2 *__restrict__ tw, int B,
                                                                      const CircRow *__restrict__ rows,
                                                                      const int32_t *__restrict__ wa,
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(128 * C, 2) void k_blind_rotate_v7_rows(const doubl
 
 // explicit CMux steps on accumulators acc [B][2][kN] with rotation amounts bara [B][iters]
 template <int C>
-__global__ __launch_bounds__(128 * C, 2) void k_blind_rotate_v7_debug(const double2 *__restrict__ bk,
+__global__ __launch_bounds__(128 * C, C == 4 ? 2 : 1) void k_blind_rotate_v7_debug(const double2 *__restrict__ bk,
                                                                       const double2 *__restrict__ tw, int B, int iters,
                                                                       int32_t *__restrict__ acc,
                                                                       const int32_t *__restrict__ bara) {
