@@ -103,6 +103,7 @@ struct V6Args {
     const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
     int prio;            // issue-priority policy, see set_prio_level
     int prio_shift;      // policy 2: steps per level = 2^prio_shift
+    int cus;             // compute units (workgroup b shares its CU with b +- cus, b +- 2 cus, ...)
 };
 
 // Issue priority.  A SIMD's two waves (different workgroups) are arbitrated by priority, then
@@ -288,6 +289,19 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         } else if (prio == 2) {
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> g.prio_shift));
+        } else if (prio == 5) {   // experiment: rank on the CU (dispatch order) sets the phase
+            if ((i & ((1 << g.prio_shift) - 1)) == 0)
+                set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
+        } else if (prio == 6) {   // experiment: SIMD partners alternate every 2^S steps
+            if ((i & ((1 << g.prio_shift) - 1)) == 0)
+                set_prio_level(((unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift)) & 1u);
+        } else if (prio == 8) {   // experiment: as 5, all four ranks of a CU on distinct levels
+            if ((i & ((1 << g.prio_shift) - 1)) == 0) {
+                const unsigned rk = (unsigned)(blockIdx.x / g.cus);
+                set_prio_level(2u * (rk & 1u) + ((rk >> 1) & 1u) + ((unsigned)i >> g.prio_shift));
+            }
+        } else if (prio == 7) {   // experiment: static, the later-dispatched partner first
+            if (i == 0) set_prio_level((unsigned)(blockIdx.x / g.cus) & 1u);
         }
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
         cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
@@ -495,6 +509,7 @@ static V6Args v6_args(const DeviceKey &key, long wgs) {
     g.prio = wgs > 0 ? v6_prio_policy(key, wgs) : 0;
     static const char *sh = getenv("TFHE_AMD_PRIO_S");
     g.prio_shift = sh ? atoi(sh) : 3;
+    g.cus = v6_cus(key);
     return g;
 }
 
