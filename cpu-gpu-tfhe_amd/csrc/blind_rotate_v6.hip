@@ -499,7 +499,7 @@ static long v6_chunk(const DeviceKey &key) {
 static int v6_prio_policy(const DeviceKey &key, long wgs) {
     static const char *env = getenv("TFHE_AMD_PRIO");
     if (env) return atoi(env);
-    return wgs > 4L * v6_cus(key) ? 1 : 2;
+    return wgs > 4L * v6_cus(key) ? 1 : 5;
 }
 
 static V6Args v6_args(const DeviceKey &key, long wgs) {
