@@ -102,17 +102,21 @@ struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
     const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
     int prio;            // issue-priority policy, see set_prio_level
-    int prio_shift;      // policy 2: steps per level = 2^prio_shift
+    int prio_shift;      // policies 2, 5: steps per level = 2^prio_shift
     int cus;             // compute units (workgroup b shares its CU with b +- cus, b +- 2 cus, ...)
 };
 
-// Issue priority.  A SIMD's two waves (different workgroups) are arbitrated by priority, then
-// age, so by default the oldest workgroup of a CU runs ahead and the youngest trails (B = 1024:
-// 2.7 ms vs 3.9 ms per workgroup, scripts/v6_wgtime.py).  Policy 1 (launches with more
-// workgroups than fit at once): priority 3 - i / 128 by step, so workgroups dispatched later,
-// still early in their 500 steps, go first (B = 4096: -11 %).  Policy 2 (one round of
-// workgroups): every 8 steps each workgroup moves to the next of the 4 levels from a hashed
-// offset, so all share the SIMDs evenly (B = 1024: -4 %).  Policy 0: hardware default.
+// Issue priority.  A SIMD holds two waves (different workgroups) and the hardware arbitrates
+// between them by priority, then age, so by default the oldest workgroup of a CU runs ahead and
+// the youngest trails (B = 1024: 2.7 ms vs 3.9 ms per workgroup, scripts/v6_wgtime.py), and
+// the launch lasts as long as the slowest.  Workgroup b shares its CU with b +- CUs, b +- 2 CUs,
+// b +- 3 CUs (dispatch order; ranks 0/1 and 2/3 share SIMD pairs).  Policy 5 (one round of
+// workgroups, the default): every 8 steps each workgroup moves one level up (mod 4) from a start
+// level 2 x rank, so SIMD partners always sit two levels apart and trade first place every 16
+// steps (B = 1024: 3.56 ms with no policy -> 3.21).  Policy 2: the same rotation from a hashed
+// start level (3.36).  Policy 1 (more workgroups than fit at once): priority 3 - i / 128 by
+// step, so workgroups dispatched later, still early in their 500 steps, go first (B = 4096 in
+// one launch: 15.4 -> 13.7 ms).  Policy 0: hardware default.  TFHE_AMD_PRIO overrides.
 __device__ __forceinline__ void set_prio_level(unsigned lvl) {
     switch (lvl & 3) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
@@ -289,19 +293,9 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         } else if (prio == 2) {
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> g.prio_shift));
-        } else if (prio == 5) {   // experiment: rank on the CU (dispatch order) sets the phase
+        } else if (prio == 5) {   // rank on the CU (dispatch order) sets the phase
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
-        } else if (prio == 6) {   // experiment: SIMD partners alternate every 2^S steps
-            if ((i & ((1 << g.prio_shift) - 1)) == 0)
-                set_prio_level(((unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift)) & 1u);
-        } else if (prio == 8) {   // experiment: as 5, all four ranks of a CU on distinct levels
-            if ((i & ((1 << g.prio_shift) - 1)) == 0) {
-                const unsigned rk = (unsigned)(blockIdx.x / g.cus);
-                set_prio_level(2u * (rk & 1u) + ((rk >> 1) & 1u) + ((unsigned)i >> g.prio_shift));
-            }
-        } else if (prio == 7) {   // experiment: static, the later-dispatched partner first
-            if (i == 0) set_prio_level((unsigned)(blockIdx.x / g.cus) & 1u);
         }
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
         cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
