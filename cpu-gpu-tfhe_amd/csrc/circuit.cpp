@@ -59,9 +59,14 @@ struct TfheAmdCircuit {
     void *d_tab = nullptr;
     int32_t *u_a = nullptr, *u_b = nullptr;
     size_t u_slots = 0;
+    StreamFence fence;   // u scratch reuse across caller streams
     ~TfheAmdCircuit() { release(); }
     void release() {
-        if (dev >= 0) (void)hipSetDevice(dev);
+        if (dev >= 0) {
+            (void)hipSetDevice(dev);
+            (void)hipDeviceSynchronize();   // a run on a caller's stream may still read them
+        }
+        fence.release();
         if (d_tab) (void)hipFree(d_tab);
         if (u_a) (void)hipFree(u_a);
         if (u_b) (void)hipFree(u_b);
@@ -322,6 +327,7 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
     }
     const size_t need = (size_t)c->max_rows * B;
     if (need > c->u_slots) {
+        (void)hipDeviceSynchronize();   // the old scratch may still be in use
         if (c->u_a) (void)hipFree(c->u_a);
         if (c->u_b) (void)hipFree(c->u_b);
         c->u_a = nullptr; c->u_b = nullptr; c->u_slots = 0;
@@ -329,6 +335,7 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
         if (hipMalloc(&c->u_b, sizeof(int32_t) * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
         c->u_slots = need;
     }
+    if (c->fence.acquire(s) != hipSuccess) return TFHE_AMD_E_HIP;
     const CircRow *d_rows = (const CircRow *)c->d_tab;
     const CircKs *d_ks = (const CircKs *)(d_rows + c->rows.size());
     const CircLin *d_lin = (const CircLin *)(d_ks + c->ks.size());
@@ -343,7 +350,7 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
         if (lv.nlin && launch_circuit_linear(B, lv.nlin, d_lin + lv.lin0, wa, wb, s) != hipSuccess)
             return TFHE_AMD_E_HIP;
     }
-    return TFHE_AMD_OK;
+    return c->fence.done(s) == hipSuccess ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
 }
 
 // ------------------------------------------------------------------ integer builders

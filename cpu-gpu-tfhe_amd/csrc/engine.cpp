@@ -130,6 +130,7 @@ struct TfheAmdContext {
     int br_n = 0, ks_n = 0;
     std::mutex mu;
     bool shared_key = false;   // lane: the key belongs to another context
+    StreamFence fence;         // u_a / u_b reuse across caller streams
 };
 
 #define HIPCHK(x)                                                                 \
@@ -175,7 +176,7 @@ int tfhe_amd_reserve(TfheAmdContext *c, int B) {
     int cap = c->cap ? c->cap : 64;
     while (cap < B) cap *= 2;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());   // the scratch may still be in use on a caller's stream
     free_scratch(c);
     HIPCHK(hipMalloc(&c->u_a, sizeof(int32_t) * 2 * (size_t)cap * kN));
     HIPCHK(hipMalloc(&c->u_b, sizeof(int32_t) * 2 * (size_t)cap));
@@ -271,9 +272,10 @@ extern "C" int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk
 extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     if (!c) return TFHE_AMD_OK;
     if (c->device >= 0) (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();   // work on caller streams may still use the scratch
     for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : c->ks_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    c->fence.release();
     free_scratch(c);
     if (!c->shared_key) free_key(c->key);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -383,6 +385,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     HIPCHK(hipSetDevice(c->device));
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
+    HIPCHK(c->fence.acquire(s));
     if (gate == TFHE_GATE_MUX) {
         if (!cc_a || !cc_b) return TFHE_AMD_E_ARG;
         // boot-gates.cu:407-448: u1 = woKS(-1/8 + a + b), u2 = woKS(-1/8 - a + c),
@@ -395,6 +398,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
         ProfScope ps(c, s, false);
         HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, c->u_a + (size_t)B * kN, c->u_b + B, kMu,
                                 res_a, res_b, s));
+        HIPCHK(c->fence.done(s));
         return TFHE_AMD_OK;
     }
     BrInput in;
@@ -406,6 +410,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
+    HIPCHK(c->fence.done(s));
     return TFHE_AMD_OK;
 }
 
@@ -431,6 +436,7 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     HIPCHK(hipSetDevice(c->device));
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
+    HIPCHK(c->fence.acquire(s));
     BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
     {
         ProfScope ps(c, s, true);
@@ -438,6 +444,7 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
+    HIPCHK(c->fence.done(s));
     return TFHE_AMD_OK;
 }
 

@@ -49,6 +49,31 @@ struct CircLin {
     int32_t c, s, in, out;
 };
 
+// Orders the reuse of a scratch buffer across streams.  Device-API callers may pass a different
+// stream per call; a call on another stream than the previous user's waits (on the device) for
+// the event recorded after that user's last launch, so two batches in flight never share the
+// extracted samples u_a / u_b.
+struct StreamFence {
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;   // compared only; the event carries the ordering
+    hipError_t acquire(hipStream_t s) const {
+        return ev && last != s ? hipStreamWaitEvent(s, ev, 0) : hipSuccess;
+    }
+    hipError_t done(hipStream_t s) {
+        if (!ev) {
+            const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        last = s;
+        return hipEventRecord(ev, s);
+    }
+    void release() {
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+        last = nullptr;
+    }
+};
+
 // BK conversion (coefficient -> NTT domain) on the device; d_bk_coef = [kn][4][2][kN]
 hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const NttTables *d_tab,
                             hipStream_t s);

@@ -1,0 +1,118 @@
+// tier1_threads.cpp — Tier-1 (single-sample TFHE C API) reentrancy and aliasing check, built
+// against include/ + libtfhe_amd only (tests/callers/Makefile).  SURVEY.md §8(b): the
+// reference's callers enter the gates from OpenMP threads (Cipher.cpp:116-120, cloud.cpp:390-393)
+// and pass a result that aliases an input (Cipher.cpp:306, 387: bootsAND(t1, t1, t2)).
+// Every gate of the API is evaluated on the same encrypted inputs three ways — sequentially,
+// from 8 OpenMP threads at once, and in place — and the three results must be the same
+// samples, word for word (the engine is deterministic); each must decrypt to its truth table.
+// Prints one JSON line; exit status 0 only when everything matched.
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include <omp.h>
+#include "tfhe/tfhe.h"
+
+typedef void (*Gate2)(LweSample *, const LweSample *, const LweSample *, const TFheGateBootstrappingCloudKeySet *);
+
+struct Gate {
+    const char *name;
+    Gate2 f;
+    int (*truth)(int, int);
+};
+
+static int t_nand(int a, int b) { return !(a & b); }
+static int t_and(int a, int b) { return a & b; }
+static int t_or(int a, int b) { return a | b; }
+static int t_xor(int a, int b) { return a ^ b; }
+static int t_xnor(int a, int b) { return !(a ^ b); }
+static int t_nor(int a, int b) { return !(a | b); }
+static int t_andny(int a, int b) { return (!a) & b; }
+static int t_andyn(int a, int b) { return a & (!b); }
+static int t_orny(int a, int b) { return (!a) | b; }
+static int t_oryn(int a, int b) { return a | (!b); }
+
+static bool same(const LweSample *x, const LweSample *y, int n) {
+    return x->b == y->b && memcmp(x->a, y->a, sizeof(Torus32) * n) == 0;
+}
+
+int main(int argc, char **argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 32;   // samples per gate
+    const Gate gates[] = {{"NAND", bootsNAND, t_nand},   {"AND", bootsAND, t_and},     {"OR", bootsOR, t_or},
+                          {"XOR", bootsXOR, t_xor},      {"XNOR", bootsXNOR, t_xnor},  {"NOR", bootsNOR, t_nor},
+                          {"ANDNY", bootsANDNY, t_andny}, {"ANDYN", bootsANDYN, t_andyn}, {"ORNY", bootsORNY, t_orny},
+                          {"ORYN", bootsORYN, t_oryn}};
+    const int ng = sizeof(gates) / sizeof(gates[0]);
+    const int units = ng + 1;   // + MUX
+
+    uint32_t seed[] = {314, 1592, 657};
+    tfhe_random_generator_setSeed(seed, 3);
+    TFheGateBootstrappingParameterSet *params = new_default_gate_bootstrapping_parameters(110);
+    TFheGateBootstrappingSecretKeySet *key = new_random_gate_bootstrapping_secret_keyset(params);
+    const TFheGateBootstrappingCloudKeySet *bk = &key->cloud;
+    const LweParams *lp = params->in_out_params;
+    const int dim = lp->n;
+
+    std::vector<int> xa(n), xb(n), xc(n);
+    uint32_t s = 12345u;
+    auto bit = [&]() { s = s * 1664525u + 1013904223u; return (int)(s >> 31); };
+    LweSample *a = new_gate_bootstrapping_ciphertext_array(n, params);
+    LweSample *b = new_gate_bootstrapping_ciphertext_array(n, params);
+    LweSample *c = new_gate_bootstrapping_ciphertext_array(n, params);
+    for (int i = 0; i < n; i++) {
+        xa[i] = bit(); xb[i] = bit(); xc[i] = bit();
+        bootsSymEncrypt(&a[i], xa[i], key);
+        bootsSymEncrypt(&b[i], xb[i], key);
+        bootsSymEncrypt(&c[i], xc[i], key);
+    }
+    const int total = units * n;
+    LweSample *seq = new_gate_bootstrapping_ciphertext_array(total, params);
+    LweSample *par = new_gate_bootstrapping_ciphertext_array(total, params);
+    LweSample *ali = new_gate_bootstrapping_ciphertext_array(total, params);
+
+    auto run = [&](int k, LweSample *out) {
+        const int g = k / n, i = k % n;
+        if (g < ng) gates[g].f(out, &a[i], &b[i], bk);
+        else bootsMUX(out, &a[i], &b[i], &c[i], bk);
+    };
+    double t0 = omp_get_wtime();
+    for (int k = 0; k < total; k++) run(k, &seq[k]);
+    double t1 = omp_get_wtime();
+#pragma omp parallel for num_threads(8) schedule(dynamic, 1)
+    for (int k = 0; k < total; k++) run(k, &par[k]);
+    double t2 = omp_get_wtime();
+    // in place: the result is the first input (even k) or the second / the MUX's c (odd k)
+#pragma omp parallel for num_threads(4) schedule(dynamic, 1)
+    for (int k = 0; k < total; k++) {
+        const int g = k / n, i = k % n;
+        LweSample *r = &ali[k];
+        if (g < ng) {
+            if (k & 1) { lweCopy(r, &b[i], lp); gates[g].f(r, &a[i], r, bk); }
+            else { lweCopy(r, &a[i], lp); gates[g].f(r, r, &b[i], bk); }
+        } else {
+            lweCopy(r, &c[i], lp);
+            bootsMUX(r, &a[i], &b[i], r, bk);
+        }
+    }
+    int par_mismatch = 0, alias_mismatch = 0, truth_errors = 0;
+    for (int k = 0; k < total; k++) {
+        const int g = k / n, i = k % n;
+        par_mismatch += !same(&seq[k], &par[k], dim);
+        alias_mismatch += !same(&seq[k], &ali[k], dim);
+        const int want = g < ng ? gates[g].truth(xa[i], xb[i]) : (xa[i] ? xb[i] : xc[i]);
+        truth_errors += bootsSymDecrypt(&seq[k], key) != want;
+    }
+    printf("{\"units\": %d, \"per_unit\": %d, \"threads\": 8, \"par_mismatch\": %d, \"alias_mismatch\": %d, "
+           "\"truth_errors\": %d, \"seq_ms_per_gate\": %.3f, \"par_ms_per_gate\": %.3f}\n",
+           units, n, par_mismatch, alias_mismatch, truth_errors, 1e3 * (t1 - t0) / total, 1e3 * (t2 - t1) / total);
+    delete_gate_bootstrapping_ciphertext_array(total, ali);
+    delete_gate_bootstrapping_ciphertext_array(total, par);
+    delete_gate_bootstrapping_ciphertext_array(total, seq);
+    delete_gate_bootstrapping_ciphertext_array(n, c);
+    delete_gate_bootstrapping_ciphertext_array(n, b);
+    delete_gate_bootstrapping_ciphertext_array(n, a);
+    delete_gate_bootstrapping_secret_keyset(key);
+    delete_gate_bootstrapping_parameters(params);
+    return par_mismatch || alias_mismatch || truth_errors ? 1 : 0;
+}
