@@ -27,8 +27,10 @@
 //    quarter of the lane's coefficients), then the FFT transposes, then the partial sum handed
 //    to the other wave; the per-lane twiddles are read from a 17 KB LDS copy (36.5 KB per
 //    ciphertext, 4 workgroups per CU), so the key is the only global load in the loop.
-//  * issue priority is steered per launch (set_prio_level): by step for multi-round launches,
-//    rotating for single-round ones.
+//  * issue priority is steered per launch (set_prio_level): a rotation phased by the workgroup's
+//    rank on its CU for the one-round launches a batch is split into (by step if the split is
+//    disabled).
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <vector>
@@ -186,7 +188,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     lds_barrier6();
     V6_STAMP(4);
     // Inverse.  Every LDS read group is issued whole before the arithmetic that consumes it
-    // (sched_barrier): at 252 VGPRs the scheduler otherwise sinks each ds_read to its use and
+    // (sched_barrier): at this register budget the scheduler otherwise sinks each ds_read to its use and
     // waits lgkmcnt(0) per pair, or per post-twist twiddle, i.e. one LDS round trip each.
     {
         Cx o[8];
@@ -471,19 +473,19 @@ hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const doub
 }
 
 // Launch geometry.  4 workgroups fit a CU (VGPRs and LDS); a launch of more than one round of
-// workgroups is split into launches of one round each (4 x CUs ciphertexts), which the
-// rotating priority policy balances: 1-2 % per step against one launch with the by-step policy
-// (B = 2048: 6.94 -> 6.80 ms, 3000: 10.13 -> 9.98, 4096: 13.47 -> 13.38; same box).
+// workgroups is split into launches of one round each (4 x CUs ciphertexts), each balanced by
+// the rank-phased rotation (policy 5): B = 4096 11.8-12.4 ms, against 13.4 with the hashed
+// rotation and >= 13.5 for one launch with the by-step policy.
 // TFHE_AMD_CHUNK=0 disables the split, TFHE_AMD_PRIO forces a policy (experiments).
 static int v6_cus(const DeviceKey &key) {
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64];   // per device; concurrent first calls store the same value
     const int d = key.device >= 0 && key.device < 64 ? key.device : 0;
-    if (!cus[d]) {
-        int n = 0;
+    int n = cus[d].load(std::memory_order_relaxed);
+    if (!n) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, key.device) != hipSuccess || n <= 0) n = 256;
-        cus[d] = n;
+        cus[d].store(n, std::memory_order_relaxed);
     }
-    return cus[d];
+    return n;
 }
 static long v6_chunk(const DeviceKey &key) {
     static const char *env = getenv("TFHE_AMD_CHUNK");

@@ -13,8 +13,9 @@
  *   LweBootstrappingKey(FFT)                  lwebootstrappingkey.h:10-59
  *   TFheGateBootstrapping{ParameterSet,CloudKeySet,SecretKeySet}
  *                                             tfhe_gate_bootstrapping_structures.h:9-63
- * TGswSampleFFT / TLweSampleFFT stay opaque: this engine keeps the bootstrapping key in
- * an exact NTT domain on the GPU instead of the reference's FFT (LagrangeHalfC) domain.
+ * TGswSampleFFT / TLweSampleFFT stay opaque: this engine keeps the bootstrapping key on the
+ * GPU in its own transform layouts (fp64 FFT for the default kernel, exact NTT for v1-v5)
+ * instead of the reference's LagrangeHalfC one.
  *
  * Semantics: synchronous, single-sample, reentrant (safe to call from
  * OpenMP threads as Cipher.cpp:116-120 does); result may alias an input; fatal errors

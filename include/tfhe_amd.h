@@ -13,7 +13,10 @@
  *   a : int32 [B][500] (row stride 500), b : int32 [B]
  * `_dev` functions take DEVICE pointers (resident in HBM) and a hipStream_t passed as
  * void* (NULL = the context's own stream); they enqueue and return (call
- * tfhe_amd_sync to wait).  `_host` functions take host pointers and are synchronous.
+ * tfhe_amd_sync to wait).  Successive calls on one context may use different streams: the
+ * engine orders the reuse of its scratch between them.  A context serves one host thread at
+ * a time (the Tier-1 API gives every calling thread its own lane).  `_host` functions take
+ * host pointers and are synchronous.
  * Every function returns 0 on success or a negative TFHE_AMD_E* code.
  */
 #ifndef TFHE_AMD_H
@@ -49,8 +52,8 @@ enum {
 
 typedef struct TfheAmdContext TfheAmdContext;
 
-/* Device context = the key material of one cloud key on one GPU: the NTT-domain
- * bootstrapping key (converted on the device from the coefficient-domain key) and the
+/* Device context = the key material of one cloud key on one GPU: the bootstrapping key in
+ * the kernels' transform domains (converted on the device from the coefficient-domain key) and the
  * key-switching key, plus a stream and scratch.  Replaces the reference's key upload
  * (gpuParallel/main.cu:165-213 sendBootstrappingKeyToGPUCoalesceExt, :236-254, :364-407). */
 int tfhe_amd_context_create(const TFheGateBootstrappingCloudKeySet *bk, int device, TfheAmdContext **out);
