@@ -8,6 +8,7 @@
 // no host round trips inside a batch; work is enqueued on a caller-chosen stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -131,6 +132,9 @@ struct TfheAmdContext {
     std::mutex mu;
     bool shared_key = false;   // lane: the key belongs to another context
     StreamFence fence;         // u_a / u_b reuse across caller streams
+    // sliced host batches (gate_batch_host_sliced): copy streams and their events
+    hipStream_t copy_in = nullptr, copy_out = nullptr;
+    hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out[2] = {nullptr, nullptr};
 };
 
 #define HIPCHK(x)                                                                 \
@@ -276,6 +280,10 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : c->ks_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     c->fence.release();
+    for (hipEvent_t e : {c->ev_in, c->ev_done, c->ev_out[0], c->ev_out[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->copy_in) (void)hipStreamDestroy(c->copy_in);
+    if (c->copy_out) (void)hipStreamDestroy(c->copy_out);
     free_scratch(c);
     if (!c->shared_key) free_key(c->key);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -478,7 +486,70 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     return TFHE_AMD_OK;
 }
 
-// host batch: stage inputs into pinned memory, one H2D, the device batch, one D2H.
+// Host batches of more than one blind-rotation round are pipelined in slices of one round:
+// slice s is computed on the context's stream while one copy stream moves slice s + 1 in and
+// another moves slice s - 1 out, and the host stages / unstages the pinned buffers meanwhile.
+// Same staging layout as below; slices touch disjoint rows, so a result that aliases an input
+// (the same array) is still read before it is written.
+static int host_slice() {   // TFHE_AMD_HOST_SLICE overrides (0: one unsliced batch)
+    static const int v = [] {
+        const char *e = getenv("TFHE_AMD_HOST_SLICE");
+        return e ? atoi(e) : 1024;
+    }();
+    return v;
+}
+
+static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
+                                  const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
+    if (!c->copy_in) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking));
+        for (hipEvent_t *e : {&c->ev_in, &c->ev_done, &c->ev_out[0], &c->ev_out[1]})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    const size_t A = (size_t)B * kn;
+    int32_t *h = c->h_io, *d = c->io, *hb = h + 4 * A, *db = d + 4 * A;
+    const int S = host_slice();
+    const int nsl = (B + S - 1) / S;
+    auto unstage = [&](int s) -> int {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
+        memcpy(res_a + (size_t)s0 * kn, h + 3 * A + (size_t)s0 * kn, (size_t)n * kn * 4);
+        memcpy(res_b + s0, hb + 3 * (size_t)B + s0, (size_t)n * 4);
+        return TFHE_AMD_OK;
+    };
+    for (int s = 0; s < nsl; ++s) {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        const size_t o = (size_t)s0 * kn, na = (size_t)n * kn;
+        for (int k = 0; k < nin; ++k) {
+            int32_t *ha = h + k * A + o, *hbk = hb + (size_t)k * B + s0;
+            memcpy(ha, in_a[k] + o, na * 4);
+            memcpy(hbk, in_b[k] + s0, (size_t)n * 4);
+            HIPCHK(hipMemcpyAsync(d + k * A + o, ha, na * 4, hipMemcpyHostToDevice, c->copy_in));
+            HIPCHK(hipMemcpyAsync(db + (size_t)k * B + s0, hbk, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_in));
+        }
+        HIPCHK(hipEventRecord(c->ev_in, c->copy_in));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
+        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, d + 3 * A + o, db + 3 * (size_t)B + s0, d + o, db + s0,
+                                               d + A + o, db + B + s0, nin > 2 ? d + 2 * A + o : nullptr,
+                                               nin > 2 ? db + 2 * (size_t)B + s0 : nullptr, c->stream);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(c->ev_done, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->copy_out, c->ev_done, 0));
+        HIPCHK(hipMemcpyAsync(h + 3 * A + o, d + 3 * A + o, na * 4, hipMemcpyDeviceToHost, c->copy_out));
+        HIPCHK(hipMemcpyAsync(hb + 3 * (size_t)B + s0, db + 3 * (size_t)B + s0, (size_t)n * 4,
+                              hipMemcpyDeviceToHost, c->copy_out));
+        HIPCHK(hipEventRecord(c->ev_out[s & 1], c->copy_out));
+        if (s > 0) {
+            const int r = unstage(s - 1);
+            if (r) return r;
+        }
+    }
+    return unstage(nsl - 1);
+}
+
+// host batch: stage inputs into pinned memory, one H2D, the device batch, one D2H (sliced and
+// pipelined above one round).
 extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                         const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
                                         const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b) {
@@ -491,6 +562,10 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     HIPCHK(hipSetDevice(c->device));
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
+    if (host_slice() > 0 && B > host_slice()) {
+        const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
+        return gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);
+    }
     const size_t A = (size_t)B * kn;
     // staging layout: [ca_a | cb_a | cc_a | res_a] then [ca_b | cb_b | cc_b | res_b]
     int32_t *h = c->h_io;

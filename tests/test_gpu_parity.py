@@ -209,6 +209,42 @@ def test_mux_split_keyswitch(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
+def test_host_batch_slices(ctx, okey, keyset, rng):
+    """Host-pointer batches above one round are pipelined in slices of 1024 over two copy
+    streams; a 3-input MUX batch of 2 100 (slices 1024 / 1024 / 52) decrypts right and matches
+    the oracle at every slice seam."""
+    B = 2100
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    r_a, r_b = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+    assert np.array_equal(keyset.decrypt(r_a, r_b), np.where(s == 1, x, y))
+    idx = np.array([0, 1023, 1024, 2047, 2048, 2099])
+    o_a, o_b = okey.gate_batch("MUX", sa[idx], sb[idx], xa[idx], xb[idx], ya[idx], yb[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+
+
+def test_large_ragged_batch(ctx, okey, keyset, rng):
+    """A batch of 12 289 gates: twelve one-round blind-rotation launches plus a ragged 13th
+    of one ciphertext, one key switch over all of them; every output decrypts right and the
+    ciphertexts at the launch seams match the oracle bit for bit."""
+    torch = _torch()
+    B = 12 * 1024 + 1
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+    dev = [torch.from_numpy(v).cuda() for v in host]
+    r_a = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    r_b = torch.empty(B, dtype=torch.int32, device="cuda")
+    ctx.reserve(B)
+    ctx.gate_dev("XNOR", r_a, r_b, *dev)
+    ctx.sync()
+    ra, rb = r_a.cpu().numpy(), r_b.cpu().numpy()
+    assert np.array_equal(keyset.decrypt(ra, rb), 1 - (x ^ y))
+    a_a, a_b, b_a, b_b = host
+    idx = np.array([0, 1023, 1024, 6143, 6144, 12287, 12288])
+    o_a, o_b = okey.gate_batch("XNOR", a_a[idx], a_b[idx], b_a[idx], b_b[idx])
+    assert np.array_equal(ra[idx], o_a) and np.array_equal(rb[idx], o_b)
+
+
 def test_scratch_reuse_across_streams(ctx, okey, keyset, rng):
     """Two device-API batches on one context from two streams, enqueued back to back with no
     host sync: the engine orders the reuse of its scratch (extracted samples) between the
