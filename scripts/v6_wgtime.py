@@ -47,6 +47,11 @@ per_cu_dur = {k: dur[key == k].mean() for k in ucu}
 for c in sorted(set(cnt)):
     ks = [k for k, m in zip(ucu, cnt) if m == c]
     print(f"    CUs with {c} WGs: mean WG duration {np.mean([per_cu_dur[k] for k in ks]):.0f} us")
+rank = np.arange(n) // 256     # dispatch rank on the CU (256 CUs: b, b+256, ... share one)
+for r_ in range(int(rank.max()) + 1 if n <= 1024 else 0):
+    m = rank == r_
+    print(f"  rank {r_}: dur med {np.median(dur[m]):.0f} p90 {np.percentile(dur[m], 90):.0f} max {dur[m].max():.0f}")
+print(f"  launch / mean duration {en.max() / dur.mean():.3f}")
 for x_ in range(8):
     m = xcc == x_
     if m.any():
