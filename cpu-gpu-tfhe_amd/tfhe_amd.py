@@ -359,9 +359,25 @@ class Context:
         return r_a, r_b
 
     # ---- device (torch) batches: tensors must be int32 CUDA/HIP tensors, contiguous
+    @staticmethod
+    def _dev_check(t, shape, name):
+        """The kernels index by shape: refuse anything that would make them read or write out
+        of bounds before it reaches the GPU."""
+        if t is None:
+            raise TfheAmdError(f"{name}: missing tensor")
+        if not t.is_cuda or t.dtype != torch.int32 or not t.is_contiguous() or tuple(t.shape) != shape:
+            raise TfheAmdError(f"{name}: need a contiguous int32 GPU tensor of shape {shape}, got "
+                               f"{tuple(t.shape)} {t.dtype} cuda={t.is_cuda} contiguous={t.is_contiguous()}")
+
     def gate_dev(self, gate, res_a, res_b, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, stream=None):
         g = GATES[gate] if isinstance(gate, str) else int(gate)
         B = ca_a.shape[0]
+        named = [("res_a", res_a, (B, n_lwe)), ("res_b", res_b, (B,)), ("ca_a", ca_a, (B, n_lwe)),
+                 ("ca_b", ca_b, (B,)), ("cb_a", cb_a, (B, n_lwe)), ("cb_b", cb_b, (B,))]
+        if g == GATES["MUX"]:
+            named += [("cc_a", cc_a, (B, n_lwe)), ("cc_b", cc_b, (B,))]
+        for name, t, shape in named:
+            self._dev_check(t, shape, name)
         ptr = (lambda t: None if t is None else t.data_ptr())
         _check(lib.tfhe_amd_gate_batch_dev(self.h, g, B, ptr(res_a), ptr(res_b), ptr(ca_a), ptr(ca_b),
                                            ptr(cb_a), ptr(cb_b), ptr(cc_a), ptr(cc_b), stream),
@@ -369,6 +385,9 @@ class Context:
 
     def blind_rotate_dev(self, acc, bara, iters, stream=None):
         B = acc.shape[0]
+        self._dev_check(acc, (B, 2, 1024), "acc")
+        if int(iters) > 0:
+            self._dev_check(bara, (B, int(iters)), "bara")
         _check(lib.tfhe_amd_blind_rotate_dev(self.h, B, int(iters), acc.data_ptr(),
                                              None if bara is None else bara.data_ptr(), stream),
                "blind_rotate_dev")

@@ -174,6 +174,24 @@ def test_chunk_boundaries_bit_exact(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
+def test_device_api_rejects_bad_tensors(ctx):
+    """Shapes, dtypes and missing MUX inputs are refused on the host, before any launch."""
+    torch = _torch()
+    B = 4
+    a = torch.zeros((B, n), dtype=torch.int32, device="cuda")
+    b = torch.zeros(B, dtype=torch.int32, device="cuda")
+    short = torch.zeros((B - 1, n), dtype=torch.int32, device="cuda")
+    with pytest.raises(T.TfheAmdError):
+        ctx.gate_dev("NAND", short, b, a, b, a, b)
+    with pytest.raises(T.TfheAmdError):
+        ctx.gate_dev("NAND", a, b, a.to(torch.int64), b, a, b)
+    with pytest.raises(T.TfheAmdError):
+        ctx.gate_dev("MUX", a, b, a, b, a, b)
+    with pytest.raises(T.TfheAmdError):
+        ctx.blind_rotate_dev(torch.zeros((B, 2, N), dtype=torch.int32, device="cuda"),
+                             torch.zeros((B, 3), dtype=torch.int32, device="cuda"), 4)
+
+
 def test_empty_batch_is_a_no_op(ctx, keyset, rng):
     torch = _torch()
     e2 = torch.empty((0, n), dtype=torch.int32, device="cuda")
