@@ -386,14 +386,16 @@ __global__ __launch_bounds__(512) void k_keyswitch_small_init(P io) {
     else if (col == kn) *ln.rb = (int32_t)ln.b;
 }
 
-template <class P>
+// U = unroll of the key-index loop: fully unrolled (16: all 128 row loads of a thread issued
+// together) for the few-ciphertext launches, 4 once several ciphertexts share the CUs
+template <class P, int U>
 __global__ __launch_bounds__(512) void k_keyswitch_small(const int32_t *__restrict__ ksk, P io) {
     const int chunk = blockIdx.x, col = threadIdx.x;
     const KsLane ln = io.lane(blockIdx.y);
     if (col > kn) return;
     const int i0 = chunk * kKsSmallI;
     uint32_t acc = 0;
-#pragma unroll 4
+#pragma unroll U
     for (int ii = 0; ii < kKsSmallI; ++ii) {
         const int i = i0 + ii;
         const uint32_t ab = (uint32_t)ln.ua[i] + (ln.ua2 ? (uint32_t)ln.ua2[i] : 0u) + kKsPrecOffset;
@@ -444,6 +446,16 @@ static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io,
     }
 }
 
+// largest key-switch count for the fully unrolled small kernel (TFHE_AMD_KS_UNROLL overrides):
+// B = 1 0.028 -> 0.021 ms, B = 64 0.110 -> 0.135 ms (measured)
+static int ks_unroll_max() {
+    static const int v = [] {
+        const char *e = getenv("TFHE_AMD_KS_UNROLL");
+        return e ? atoi(e) : 8;
+    }();
+    return v;
+}
+
 // largest key-switch count that takes the small-batch kernels (TFHE_AMD_KS_SMALL overrides)
 static int ks_small_max() {
     static const int v = [] {
@@ -459,7 +471,12 @@ hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const Cir
     KsRows io{ks, u_a, u_b, wa, wb, B, nks};
     if ((long)B * nks <= ks_small_max()) {
         hipLaunchKernelGGL(k_keyswitch_small_init<KsRows>, dim3(B * nks), dim3(512), 0, s, io);
-        hipLaunchKernelGGL(k_keyswitch_small<KsRows>, dim3(kKsSmallChunks, B * nks), dim3(512), 0, s, key.ksk, io);
+        if ((long)B * nks <= ks_unroll_max())
+            hipLaunchKernelGGL((k_keyswitch_small<KsRows, kKsSmallI>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
+                               key.ksk, io);
+        else
+            hipLaunchKernelGGL((k_keyswitch_small<KsRows, 4>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
+                               key.ksk, io);
         return hipGetLastError();
     }
     const int groups = (int)(((size_t)B * nks + kKs4Threads - 1) / kKs4Threads);
@@ -524,7 +541,11 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
     } else if (B <= ks_small_max()) {
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
         hipLaunchKernelGGL(k_keyswitch_small_init<KsPlain>, dim3(B), dim3(512), 0, s, io);
-        hipLaunchKernelGGL(k_keyswitch_small<KsPlain>, dim3(kKsSmallChunks, B), dim3(512), 0, s, key.ksk, io);
+        if (B <= ks_unroll_max())
+            hipLaunchKernelGGL((k_keyswitch_small<KsPlain, kKsSmallI>), dim3(kKsSmallChunks, B), dim3(512), 0, s,
+                               key.ksk, io);
+        else
+            hipLaunchKernelGGL((k_keyswitch_small<KsPlain, 4>), dim3(kKsSmallChunks, B), dim3(512), 0, s, key.ksk, io);
     } else {
         const int groups = (B + kKs4Threads - 1) / kKs4Threads;
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
