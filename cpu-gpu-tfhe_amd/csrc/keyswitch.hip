@@ -387,7 +387,12 @@ __global__ __launch_bounds__(512) void k_keyswitch_small_init(P io) {
 }
 
 // U = unroll of the key-index loop: fully unrolled (16: all 128 row loads of a thread issued
-// together) for the few-ciphertext launches, 4 once several ciphertexts share the CUs
+// together) for the few-ciphertext launches, kKsSmallU once several ciphertexts share the CUs
+// (2: B = 16..96 -10..12 % against 4; 1 measured the same as 2, 8 in between)
+#ifndef TFHE_AMD_KS_SMALL_U
+#define TFHE_AMD_KS_SMALL_U 2
+#endif
+constexpr int kKsSmallU = TFHE_AMD_KS_SMALL_U;
 template <class P, int U>
 __global__ __launch_bounds__(512) void k_keyswitch_small(const int32_t *__restrict__ ksk, P io) {
     const int chunk = blockIdx.x, col = threadIdx.x;
@@ -447,11 +452,11 @@ static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io,
 }
 
 // largest key-switch count for the fully unrolled small kernel (TFHE_AMD_KS_UNROLL overrides):
-// B = 1 0.028 -> 0.021 ms, B = 64 0.110 -> 0.135 ms (measured)
+// B = 1 0.028 -> 0.021 ms; at B = 8 the 2-way unroll is already faster (0.029 vs 0.031 ms)
 static int ks_unroll_max() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_KS_UNROLL");
-        return e ? atoi(e) : 8;
+        return e ? atoi(e) : 4;
     }();
     return v;
 }
@@ -475,7 +480,7 @@ hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const Cir
             hipLaunchKernelGGL((k_keyswitch_small<KsRows, kKsSmallI>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
                                key.ksk, io);
         else
-            hipLaunchKernelGGL((k_keyswitch_small<KsRows, 4>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
+            hipLaunchKernelGGL((k_keyswitch_small<KsRows, kKsSmallU>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
                                key.ksk, io);
         return hipGetLastError();
     }
@@ -545,7 +550,8 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
             hipLaunchKernelGGL((k_keyswitch_small<KsPlain, kKsSmallI>), dim3(kKsSmallChunks, B), dim3(512), 0, s,
                                key.ksk, io);
         else
-            hipLaunchKernelGGL((k_keyswitch_small<KsPlain, 4>), dim3(kKsSmallChunks, B), dim3(512), 0, s, key.ksk, io);
+            hipLaunchKernelGGL((k_keyswitch_small<KsPlain, kKsSmallU>), dim3(kKsSmallChunks, B), dim3(512), 0, s,
+                               key.ksk, io);
     } else {
         const int groups = (B + kKs4Threads - 1) / kKs4Threads;
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
