@@ -218,9 +218,13 @@ __global__ __launch_bounds__(kKsV2Threads) void k_keyswitch_v3(
 constexpr int kKs4Cols = 4;
 constexpr int kKs4Blocks = 126;                 // ceil(501 / 4)
 constexpr int kKs4I = 32;                       // key indices per chunk
-constexpr int kKs4Threads = 256;
+#ifndef TFHE_AMD_KS4_THREADS
+#define TFHE_AMD_KS4_THREADS 256
+#endif
+constexpr int kKs4Threads = TFHE_AMD_KS4_THREADS;   // = ciphertexts per workgroup
 constexpr int kKs4ChunkU4 = kKs4I * kKsT * 3;   // uint4 pieces per chunk = 768
 static_assert(kKs4ChunkU4 % kKs4Threads == 0, "chunk must split evenly");
+constexpr int kKs4Pieces = kKs4ChunkU4 / kKs4Threads;   // per thread and chunk
 
 // Where lane ct of the key switch reads and writes (gate batches and circuit levels).
 struct KsLane {
@@ -299,22 +303,25 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
     const uint4 *src = ksk4 + ((size_t)cb * kN + ibeg) * kKsT * 3 + tid;
     const uint4 *pa = reinterpret_cast<const uint4 *>(ln.ua + ibeg);
     const uint4 *pa2 = ln.ua2 ? reinterpret_cast<const uint4 *>(ln.ua2 + ibeg) : nullptr;
-    // (i, j, h - 1) piece t = tid + 256 l of a chunk goes to buf[.][(t / 3) * 4 + t % 3 + 1]
-    int dst[3];
+    // (i, j, h - 1) piece t = tid + threads l of a chunk goes to buf[.][(t / 3) * 4 + t % 3 + 1]
+    int dst[kKs4Pieces];
+    uint4 p[kKs4Pieces];
 #pragma unroll
-    for (int l = 0; l < 3; ++l) {
+    for (int l = 0; l < kKs4Pieces; ++l) {
         const int t = tid + kKs4Threads * l;
         dst[l] = (t / 3) * 4 + (t - 3 * (t / 3)) + 1;
     }
-    // register prefetch of one chunk: 3 KSK pieces + this lane's 32 a-values (+ u2's)
-    uint4 p0 = src[0], p1 = src[kKs4Threads], p2 = src[2 * kKs4Threads];
+    // register prefetch of one chunk: the KSK pieces + this lane's 32 a-values (+ u2's)
+#pragma unroll
+    for (int l = 0; l < kKs4Pieces; ++l) p[l] = src[kKs4Threads * l];
     uint4 av[kKs4I / 4], av2[kKs4I / 4];
 #pragma unroll
     for (int v = 0; v < kKs4I / 4; ++v) {
         av[v] = pa[v];
         av2[v] = pa2 ? pa2[v] : make_uint4(0, 0, 0, 0);
     }
-    buf[0][dst[0]] = p0; buf[0][dst[1]] = p1; buf[0][dst[2]] = p2;
+#pragma unroll
+    for (int l = 0; l < kKs4Pieces; ++l) buf[0][dst[l]] = p[l];
     __syncthreads();
     for (int i0 = 0, b = 0; i0 < kIPart; i0 += kKs4I, b ^= 1) {
         uint32_t a[kKs4I];
@@ -328,7 +335,8 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
         const bool more = i0 + kKs4I < kIPart;
         if (more) {                                          // next chunk, in flight during the gather
             const uint4 *sn = src + (size_t)(i0 + kKs4I) * kKsT * 3;
-            p0 = sn[0]; p1 = sn[kKs4Threads]; p2 = sn[2 * kKs4Threads];
+#pragma unroll
+            for (int l = 0; l < kKs4Pieces; ++l) p[l] = sn[kKs4Threads * l];
 #pragma unroll
             for (int v = 0; v < kKs4I / 4; ++v) {
                 av[v] = pa[(i0 + kKs4I) / 4 + v];
@@ -351,7 +359,8 @@ __global__ __launch_bounds__(kKs4Threads) void k_keyswitch_v4(const uint4 *__res
         }
         if (more) {                                          // other buffer: last read one chunk ago
             uint4 *nb = buf[b ^ 1];
-            nb[dst[0]] = p0; nb[dst[1]] = p1; nb[dst[2]] = p2;
+#pragma unroll
+            for (int l = 0; l < kKs4Pieces; ++l) nb[dst[l]] = p[l];
         }
         __syncthreads();
     }
