@@ -9,23 +9,31 @@ rank processes its own shard of independent ciphertexts; no collective on the da
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
 Rank 0 prints ONE JSON line.  Extra objects:
-  roofline     : SURVEY.md §8(d)'s figure for the dominant kernel (the blind rotation): its
-                 algorithmic key-stream bytes (32 768 000 B of TGSW key per bootstrap, NTT or
-                 FFT domain alike) x B / its average time per batch (HIP events the engine
-                 records around every launch, on the stream it launches on, live over the K
-                 timed steps; one launch per 1024 ciphertexts) vs the 8 TB/s HBM peak;
-                 `traffic` = the HBM bytes per launch from the profiles/ PMC data.  Every ciphertext of the batch streams the same key slice
-                 per step, so the reads are L2/MALL hits and `frac` can exceed 1; the kernel is
-                 in fact bound by fp64 VALU issue, which `roofline.compute` reports: its
-                 algorithmic fp64 FLOPs (198 656 per CMux step, FMA = 2) / launch time vs the
-                 78.6 TFLOP/s fp64 vector peak.
-  cpu_baseline : the CPU restatement (oracle/, same algorithm, exact NTT, OpenMP) timed on
-                 this host's cores on a bounded sample of the same workload (rank 0, N=1).
+  roofline     : the dominant kernel (the blind rotation) against the roofline that binds it,
+                 fp64 VALU issue: its algorithmic fp64 FLOPs (198 656 per CMux step, FMA = 2,
+                 x 500 steps x B) / its average launch time (HIP events the engine records
+                 around every launch, on the stream it launches on, live over the K timed steps)
+                 vs the 78.6 TFLOP/s fp64 vector peak.  `traffic` = HBM bytes per launch from
+                 the committed rocprofv3 PMC passes (profiles/pmc_summary.json).
+                 `hbm` is SURVEY.md §8(d)'s key-stream view of the same launch: the measured
+                 HBM bytes (PMC) / launch time vs 8 TB/s, next to the streaming model's
+                 algorithmic bytes (every ciphertext streaming the 32.768 MB key; the batch
+                 shares each key slice through L2, so those are cache hits, not HBM reads).
+                 `clock` = the shader clock sampled during a sustained run (amd-smi), and the
+                 fp64 fraction at that clock.
+  batches      : the same step at B = 1 and 4096 per GPU (BASELINE metric's other batch sizes)
+  strong       : global batch 4096 split over the ranks (BASELINE: batch 4096 on 1..8 GPUs)
+  cpu_baseline : the optimized CPU port (oracle/cpu_fft.c: fp64 FFT external product, the
+                 spqlios algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to
+                 the exact oracle) timed on this host's cores on a bounded sample (rank 0, N=1),
+                 with its single-core ms per bootstrap and the host CPU model.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -33,16 +41,18 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "cpu-gpu-tfhe_amd"))
 
-BK_BYTES_PER_BOOTSTRAP = 500 * 4 * 2 * 1024 * 8        # NTT-domain TGSW key stream, 32 768 000 B
+BK_BYTES_PER_BOOTSTRAP = 500 * 4 * 2 * 1024 * 8        # FFT/NTT-domain TGSW key stream, 32 768 000 B
 KS_BYTES_PER_KEYSWITCH = 1024 * 8 * 501 * 4            # KSK rows, 16 416 768 B
+IO_BYTES_PER_GATE = 2 * 2004 + 4100                    # two LWE inputs read + one extracted sample written
 HBM_PEAK_GBPS = 8000.0
-# v6 fp64 work per CMux step (blind_rotate_v6.hip; DESIGN.md §5.1c), FMA = 2: 4 forward
+# v6 fp64 work per CMux step (blind_rotate_v6.hip; DESIGN.md §3.1), FMA = 2: 4 forward
 # transforms x 2304 butterflies x 12 + 2 inverse (640 trivial butterflies x 4 + 1664 x 12 +
 # 512-point post-twist x 6) + MAC 2 x 4 x 512 x 7 + partial sums 2048 + mod-2^32 rounding 2048 x 3
 INV_FLOPS = 640 * 4 + 1664 * 12 + 512 * 6
 FLOPS_PER_CMUX = 4 * 2304 * 12 + 2 * INV_FLOPS + 2 * 4 * 512 * 7 + 2048 + 2048 * 3   # 198 656
 FLOPS_PER_BOOTSTRAP = 500 * FLOPS_PER_CMUX
-FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP), AMD spec
+FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP) at the 2.4 GHz peak clock
+PEAK_CLOCK_MHZ = 2400.0
 
 
 def parse():
@@ -52,32 +62,76 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
+    ap.add_argument("--extra-batches", default="1,4096", help="per-GPU batch sizes also timed ('' = none)")
+    ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------------------- CPU side
+
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity}
+
+
+def cpu_threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(bk, ksk, rng, target_s):
-    """Oracle (CPU port of the reference path, exact NTT) on all available host threads."""
+    """The optimized CPU port (oracle/cpu_fft.c) on the host threads this process may use
+    (OMP_NUM_THREADS, else its CPU affinity): ~target_s of work, plus a single-thread sample."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ctypes as O
-    okey = O.OracleKey(bk, ksk, use_ntt=True)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or O.max_threads()
+    fk = O.CpuFftKey(bk, ksk)
+    threads = cpu_threads()
     n = 500
 
-    def run(B):
+    def run(B, th):
         a = rng.integers(-2**31, 2**31, (B, n), dtype=np.int64).astype(np.int32)
         b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
         t0 = time.perf_counter()
-        okey.gate_batch("NAND", a, b, a[::-1].copy(), b[::-1].copy(), nthreads=threads)
+        fk.gate_batch("NAND", a, b, a[::-1].copy(), b[::-1].copy(), nthreads=th)
         return time.perf_counter() - t0
 
-    t1 = run(threads)                      # warm-up + rate estimate: one gate per thread
-    B = max(threads, int(target_s / max(t1, 1e-3)) * threads)
-    t = run(B)
-    return {"value": B / t, "unit": "gate bootstraps/s", "cores": threads, "kind": "port",
-            "sample": f"{B} bootsNAND (random LWE inputs) on {threads} OpenMP threads, {t:.1f} s"}
+    run(threads, threads)                  # warm-up (thread team, key pages)
+    t1 = run(2 * threads, threads)         # rate estimate
+    B = max(threads, int(target_s / max(t1 / 2, 1e-3)) * threads)
+    t = run(B, threads)
+    run(1, 1)
+    single = min(run(4, 1) / 4 for _ in range(2))
+    out = {"value": B / t, "unit": "gate bootstraps/s", "cores": threads, "kind": "port",
+           "sample": f"{B} bootsNAND (random LWE inputs) on {threads} OpenMP threads, {t:.1f} s",
+           "engine": "optimized fp64-FFT port of the reference CPU path (oracle/cpu_fft.c; spqlios "
+                     "algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to the exact oracle)",
+           "single_core_ms_per_bootstrap": single * 1e3,
+           "paper_single_core_ms_per_gate": 43.8,
+           "max_round_error": fk.max_round_error()}
+    out.update(host_info())
+    return out
 
+
+# ------------------------------------------------------------------------------- GPU side
 
 def pmc_traffic(engine, batch):
     """HBM bytes per blind-rotation launch from the committed rocprofv3 PMC summary
@@ -88,11 +142,65 @@ def pmc_traffic(engine, batch):
     try:
         s = json.load(open(path))
     except (OSError, ValueError):
-        return None
+        return None, None
     k = s.get("kernels", {}).get("blind_rotate")
     if not k or s.get("engine") != engine or s.get("batch") != batch:
+        return None, None
+    return k["hbm_bytes_per_launch"], s.get("source")
+
+
+def _gfx_clock_mhz(obj):
+    """Current GFX clock(s) from `amd-smi metric --clock --json` (tolerant walk)."""
+    vals = []
+
+    def walk(o, path):
+        if isinstance(o, dict):
+            for k, v in o.items():
+                walk(v, path + [str(k).lower()])
+        elif isinstance(o, list):
+            for v in o:
+                walk(v, path)
+        else:
+            p = "/".join(path)
+            if "gfx" in p and ("clk" in p or "clock" in p) and "min" not in p and "max" not in p \
+                    and "lock" not in p.replace("clock", "") and ("cur" in p or p.endswith("clk/value")):
+                try:
+                    vals.append(float(o))
+                except (TypeError, ValueError):
+                    pass
+    walk(obj, [])
+    return vals
+
+
+def sample_clock(device, run_step, seconds=2.0):
+    """Shader clock under the bench's own sustained load: steps run back to back on the GPU
+    while another thread samples amd-smi.  Returns {"mhz": median, "samples": n} or None."""
+    samples = []
+    stop = threading.Event()
+
+    def poll():
+        while not stop.is_set():
+            try:
+                r = subprocess.run(["amd-smi", "metric", "-g", str(device), "--clock", "--json"],
+                                   capture_output=True, text=True, timeout=10)
+                v = _gfx_clock_mhz(json.loads(r.stdout)) if r.returncode == 0 and r.stdout.strip() else []
+                v = [x for x in v if 100.0 < x < 5000.0]
+                if v:
+                    samples.append(sum(v) / len(v))
+            except Exception:   # no amd-smi / unparsable output: no clock figure
+                return
+    th = threading.Thread(target=poll, daemon=True)
+    t_end = time.perf_counter() + seconds
+    run_step()
+    th.start()
+    while time.perf_counter() < t_end:
+        run_step()
+    stop.set()
+    th.join(timeout=15)
+    if not samples:
         return None
-    return k["hbm_bytes_per_launch"]
+    samples.sort()
+    return {"mhz": samples[len(samples) // 2], "samples": len(samples)}
 
 
 def main():
@@ -122,60 +230,83 @@ def main():
 
     K = T.SecretKeyset()                   # real keys (seed 314,1592,657), ~1 s on the host
     rng = np.random.default_rng(1000 + rank)
-    B = args.batch
-    x = rng.integers(0, 2, B)
-    y = rng.integers(0, 2, B)
-    a_a, a_b = K.encrypt(x, rng)
-    b_a, b_b = K.encrypt(y, rng)
-    dev = [torch.from_numpy(v).cuda() for v in (a_a, a_b, b_a, b_b)]
-    r_a = torch.empty((B, 500), dtype=torch.int32, device="cuda")
-    r_b = torch.empty(B, dtype=torch.int32, device="cuda")
     ctx = T.Context(K.bk, K.ksk, device=local)
-    ctx.reserve(B)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step():
-        ctx.gate_dev(args.gate, r_a, r_b, *dev, stream=stream)
+    def make_batch(B):
+        x = rng.integers(0, 2, B)
+        y = rng.integers(0, 2, B)
+        a_a, a_b = K.encrypt(x, rng)
+        b_a, b_b = K.encrypt(y, rng)
+        dev = [torch.from_numpy(v).cuda() for v in (a_a, a_b, b_a, b_b)]
+        r_a = torch.empty((B, 500), dtype=torch.int32, device="cuda")
+        r_b = torch.empty(B, dtype=torch.int32, device="cuda")
+        ctx.reserve(B)
+        return x, y, dev, r_a, r_b
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # kernel timing for the roofline: HIP events around each engine launch, recorded by the
-    # engine on the stream it launches on, live over the timed steps
-    ctx.profile_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=red_dev)
-    prof = ctx.profile_read()
-    ctx.profile_enable(False)
+    def timed(B, steps, warmup, profile=False):
+        """W warmup + K timed steps of batch B, barrier + synchronize on both sides, max over
+        ranks; returns (elapsed_s, profile dict, truth_ok)."""
+        x, y, dev, r_a, r_b = make_batch(B)
 
-    # correctness guard on the last step's output (truth table; cheap)
-    dec = K.decrypt(r_a.cpu().numpy(), r_b.cpu().numpy())
-    truth_ok = bool(np.array_equal(dec, 1 - (x & y))) if args.gate == "NAND" else None
+        def step():
+            if B > 0:
+                ctx.gate_dev(args.gate, r_a, r_b, *dev, stream=stream)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if profile:
+            # kernel timing for the roofline: HIP events around each engine launch, recorded by
+            # the engine on the stream it launches on, live over the timed steps
+            ctx.profile_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = shard.max_over_ranks(time.perf_counter() - t0, device=red_dev)
+        prof = None
+        if profile:
+            prof = ctx.profile_read()
+            ctx.profile_enable(False)
+        ok = None
+        if args.gate == "NAND" and B > 0:
+            dec = K.decrypt(r_a.cpu().numpy(), r_b.cpu().numpy())
+            ok = bool(np.array_equal(dec, 1 - (x & y)))
+        return el, prof, ok, step
+
+    B = args.batch
+    elapsed, prof, truth_ok, main_step = timed(B, args.steps, args.warmup, profile=True)
 
     br_ms = prof["br_ms"] / max(1, prof["br_launches"])
     ks_ms = prof["ks_ms"] / max(1, prof["ks_launches"])
-    key_gbps = B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9
     fft = "fft64" in T.version()
-    roof = {"bound": "hbm", "achieved": key_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": key_gbps / HBM_PEAK_GBPS, "traffic": pmc_traffic(T.version(), B),
-            "kernel": "k_blind_rotate_v" + T.version().split("br-v")[1].split(" ")[0], "kernel_ms": br_ms,
-            "keyswitch_ms": ks_ms, "algorithmic_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP,
-            "note": "achieved counts every ciphertext's full key stream; the batch shares each key "
-                    "slice through L2 (hit rate 99 %), so frac > 1 is possible and traffic (real HBM "
-                    "bytes) is ~1 % of it; the kernel is SIMD-bound, see compute (DESIGN.md 5.1)"}
+    kernel = "k_blind_rotate_v" + T.version().split("br-v")[1].split(" ")[0]
+    traffic, traffic_src = pmc_traffic(T.version(), B)
+    unique = BK_BYTES_PER_BOOTSTRAP + B * IO_BYTES_PER_GATE
+    hbm = {"achieved": None if traffic is None else traffic / (br_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
+           "unit": "GB/s", "frac": None if traffic is None else traffic / (br_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+           "traffic_bytes_per_launch": traffic, "traffic_source": traffic_src,
+           "unique_bytes_per_launch": unique,
+           "refetch_ratio": None if traffic is None else traffic / unique,
+           "streaming_model_bytes_per_launch": B * BK_BYTES_PER_BOOTSTRAP,
+           "streaming_model_GBps": B * BK_BYTES_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e9,
+           "note": "traffic = HBM bytes from PMC FETCH_SIZE (x2, gfx950) + WRITE_SIZE per launch; "
+                   "refetch_ratio = traffic / (key once + ciphertext I/O): each XCD's L2 refills the "
+                   "key; the streaming model counts every ciphertext's key stream, served from L2"}
     if fft:
         tflops = B * FLOPS_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e12
-        roof["compute"] = {"bound": "valu-fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS,
-                           "unit": "TFLOP/s", "frac": tflops / FP64_PEAK_TFLOPS,
-                           "flops_per_launch": B * FLOPS_PER_BOOTSTRAP}
+        roof = {"bound": "valu-fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel, "kernel_ms": br_ms,
+                "keyswitch_ms": ks_ms, "flops_per_launch": B * FLOPS_PER_BOOTSTRAP,
+                "flops_per_cmux_step": FLOPS_PER_CMUX, "hbm": hbm}
+    else:   # exact-NTT generations: integer VALU bound; report the key-stream view only
+        roof = {"bound": "valu-int", "achieved": None, "peak": None, "unit": None, "frac": None,
+                "traffic": traffic, "kernel": kernel, "kernel_ms": br_ms, "keyswitch_ms": ks_ms, "hbm": hbm}
 
     value = shard.weak_scaling_value(B, world, args.steps, elapsed)
     line = {
@@ -199,8 +330,43 @@ def main():
         "truth_table_ok": truth_ok,
         "engine": T.version(),
     }
+
+    # clock under this load (rank 0 samples its own GPU; other ranks keep their GPUs busy too)
+    if not args.no_clock and fft:
+        clk = sample_clock(local, main_step)
+        torch.cuda.synchronize()
+        if clk:
+            held = FP64_PEAK_TFLOPS * clk["mhz"] / PEAK_CLOCK_MHZ
+            roof["clock"] = {"gfx_mhz": clk["mhz"], "samples": clk["samples"],
+                             "fp64_peak_at_clock": held, "frac_at_clock": roof["achieved"] / held}
+    if world > 1:
+        dist.barrier()
+
+    # the metric's other batch sizes (per GPU, weak scaling like the headline)
+    extras = {}
+    for s in (v for v in args.extra_batches.split(",") if v.strip()):
+        b = int(s)
+        if b == B or b <= 0:
+            continue
+        steps = max(3, min(args.steps, int(200 / b) + 5)) if b < 64 else max(3, args.steps // 2)
+        el, pr, ok, _ = timed(b, steps, 1, profile=True)
+        extras[str(b)] = {"value": shard.weak_scaling_value(b, world, steps, el), "ms_per_step": el / steps * 1e3,
+                          "steps": steps, "kernel_ms": pr["br_ms"] / max(1, pr["br_launches"]),
+                          "keyswitch_ms": pr["ks_ms"] / max(1, pr["ks_launches"]), "truth_table_ok": ok}
+    if extras:
+        line["batches"] = extras
+    # strong scaling of one global batch over the ranks (contiguous shards, shard.py)
+    if args.strong_batch > 0:
+        lo, hi = shard.shard_range(args.strong_batch, rank, world)
+        steps = max(3, args.steps // 2)
+        el, _, ok, _ = timed(hi - lo, steps, 1)
+        line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
+                          "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
+                          "steps": steps, "truth_table_ok": ok}
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(K.bk, K.ksk, np.random.default_rng(5), args.cpu_seconds)
+        line["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -155,3 +155,70 @@ class OracleKey:
 
 def max_threads():
     return int(lib().orc_max_threads())
+
+
+# --------------------------------------------------------------------- optimized CPU baseline
+CPUFFT_SO = os.path.join(ORACLE_DIR, "libcpufft.so")
+_fft = None
+
+
+def fftlib():
+    global _fft
+    if _fft is None:
+        if not os.path.exists(CPUFFT_SO):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = ctypes.CDLL(CPUFFT_SO)
+        L.cpufft_key_create.restype = ctypes.c_void_p
+        L.cpufft_key_create.argtypes = [_I32P, _I32P]
+        L.cpufft_key_free.argtypes = [ctypes.c_void_p]
+        L.cpufft_max_round_error.restype = ctypes.c_double
+        L.cpufft_max_round_error.argtypes = [ctypes.c_void_p]
+        L.cpufft_gate_batch.restype = None
+        L.cpufft_gate_batch.argtypes = [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32] + [_I32P] * 6 \
+            + [ctypes.c_void_p, ctypes.c_int]
+        L.cpufft_woks_batch.restype = None
+        L.cpufft_woks_batch.argtypes = [ctypes.c_int, _I32P, _I32P, ctypes.c_void_p, ctypes.c_int32, _I32P, _I32P,
+                                        ctypes.c_int]
+        _fft = L
+    return _fft
+
+
+# gate prologue constants (boot-gates.cu:98-397), as the product's gate_spec
+GATE_SPEC = {"NAND": (1 << 29, -1, -1), "OR": (1 << 29, 1, 1), "AND": (-(1 << 29), 1, 1),
+             "XOR": (1 << 30, 2, 2), "XNOR": (-(1 << 30), -2, -2), "NOR": (-(1 << 29), -1, -1),
+             "ANDNY": (-(1 << 29), -1, 1), "ANDYN": (-(1 << 29), 1, -1), "ORNY": (1 << 29, -1, 1),
+             "ORYN": (1 << 29, 1, -1)}
+
+
+class CpuFftKey:
+    """The optimized CPU baseline engine (oracle/cpu_fft.c): fp64 FFT external product,
+    OpenMP over gates.  Borrows ksk."""
+
+    def __init__(self, bk, ksk):
+        self.bk = i32(bk)
+        self.ksk = i32(ksk)
+        self.h = fftlib().cpufft_key_create(_p(self.bk), _p(self.ksk))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            fftlib().cpufft_key_free(self.h)
+            self.h = None
+
+    def max_round_error(self):
+        return fftlib().cpufft_max_round_error(self.h)
+
+    def gate_batch(self, gate, ca_a, ca_b, cb_a, cb_b, nthreads=0):
+        c, sa, sb = GATE_SPEC[gate]
+        ca_a = i32(ca_a); B = ca_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32)
+        r_b = np.zeros(B, np.int32)
+        fftlib().cpufft_gate_batch(B, c, sa, sb, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)), _p(i32(cb_a)),
+                                   _p(i32(cb_b)), self.h, int(nthreads))
+        return r_a, r_b
+
+    def woks_batch(self, mu, x_a, x_b, nthreads=0):
+        x_a = i32(x_a); B = x_a.shape[0]
+        o_a = np.zeros((B, N), np.int32)
+        o_b = np.zeros(B, np.int32)
+        fftlib().cpufft_woks_batch(B, _p(o_a), _p(o_b), self.h, int(mu), _p(x_a), _p(i32(x_b)), int(nthreads))
+        return o_a, o_b
