@@ -6,10 +6,15 @@
 // Prints one JSON line with the decrypted results of the reference's circuits:
 //   a + b (operator+, Cipher.cpp ripple-carry with addBits), a - b (twosComplement + add),
 //   a * b (operator*, shift-and-add; on the low 8 bits), minimum(a, b), a == b, a > b.
-// Integration test only (tests/test_io.py::test_reference_callers_gpu).
+// `cipher_ops add32 A B`: BASELINE config 3 through the unchanged Cipher::operator+
+// (Cipher.cpp:348-392, 5 gates per bit) on 32-bit operands encrypted here with
+// bootsSymEncrypt under secret.key; prints {"a", "b", "sum", "seconds"}.
+// Integration tests only (tests/test_io.py::test_reference_callers_gpu,
+// tests/test_configs_gpu.py::test_config3_cipher_operator_plus_32bit).
 #include <cstdio>
 #include <cstdlib>
 #include <omp.h>
+#include <string>
 
 #include "Cipher.h"
 
@@ -19,11 +24,30 @@ static long decode(const Cipher &c, const TFheGateBootstrappingSecretKeySet *key
     return v;
 }
 
-int main() {
+static int add32(const TFheGateBootstrappingSecretKeySet *key, long av, long bv) {
+    const TFheGateBootstrappingParameterSet *params = Cipher::bk->params;
+    const int bits = 32;
+    LweSample *x = new_gate_bootstrapping_ciphertext_array(bits, params);
+    LweSample *y = new_gate_bootstrapping_ciphertext_array(bits, params);
+    for (int i = 0; i < bits; i++) {
+        bootsSymEncrypt(&x[i], (int)((av >> i) & 1), key);
+        bootsSymEncrypt(&y[i], (int)((bv >> i) & 1), key);
+    }
+    Cipher a(bits, x), b(bits, y);
+    double t0 = omp_get_wtime();
+    Cipher sum = a + b;
+    double t1 = omp_get_wtime();
+    printf("{\"a\": %ld, \"b\": %ld, \"sum\": %ld, \"seconds\": %.4f}\n", decode(a, key), decode(b, key),
+           decode(sum, key), t1 - t0);
+    return 0;
+}
+
+int main(int argc, char **argv) {
     FILE *f = fopen("secret.key", "rb");
     if (!f) { fprintf(stderr, "secret.key missing\n"); return 2; }
     TFheGateBootstrappingSecretKeySet *key = new_tfheGateBootstrappingSecretKeySet_fromFile(f);
     fclose(f);
+    if (argc == 4 && std::string(argv[1]) == "add32") return add32(key, atol(argv[2]), atol(argv[3]));
     const TFheGateBootstrappingParameterSet *params = Cipher::bk->params;
     const int bits = 16;
     LweSample *x = new_gate_bootstrapping_ciphertext_array(bits, params);

@@ -1,0 +1,172 @@
+"""BASELINE.json configs at their stated sizes on the MI355X (through the C ABI), each
+decrypted against integer arithmetic and, where the oracle can afford
+it, compared Torus32 bit for bit (P1):
+
+  configs[1]: 1024 independent bootsNAND — ALL 1024 outputs bit-exact vs the oracle; the
+              4096 batch of the metric: every launch seam plus a 256-sample bit-exact;
+  configs[2]: one 32-bit ripple-carry addition, through the circuit API and through the
+              reference's unchanged Cipher::operator+ (cpuParallel/Cipher.cpp:348-392);
+  configs[3]: 16 x 16-bit multiplication, batch 256 (multiplication.cu circuit's size);
+  configs[4]: rows of the 64 x 64 16-bit matrix-vector product (matrixUtility path);
+plus a Torus32 check of the circuit-row kernel (k_blind_rotate_v6_rows) against the oracle
+for the three-input MAJ / XOR3 rows and the prefix adder's 2/1/1 threshold row."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import matvec
+import tfhe_amd as T
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CALLERS = os.path.join(REPO, "oracle", "_ref", "callers")
+N, n = 1024, 500
+E8 = 1 << 29
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+def _gate_dev(ctx, gate, host):
+    torch = _torch()
+    B = host[0].shape[0]
+    dev = [torch.from_numpy(v).cuda() for v in host]
+    r_a = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    r_b = torch.empty(B, dtype=torch.int32, device="cuda")
+    ctx.reserve(B)
+    ctx.gate_dev(gate, r_a, r_b, *dev)
+    ctx.sync()
+    return r_a.cpu().numpy(), r_b.cpu().numpy()
+
+
+def test_config1_batch_1024_all_bit_exact(ctx, okey, keyset, rng):
+    """configs[1]: every one of the 1024 gates equals the oracle word for word."""
+    B = 1024
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+    ra, rb = _gate_dev(ctx, "NAND", host)
+    assert np.array_equal(keyset.decrypt(ra, rb), 1 - (x & y))
+    oa, ob = okey.gate_batch("NAND", *host)
+    assert np.array_equal(ra, oa) and np.array_equal(rb, ob)
+
+
+def test_metric_batch_4096_seams_and_sample(ctx, okey, keyset, rng):
+    """The metric's batch 4096 (four one-round launches of 1024): truth table on all, the
+    ciphertexts at every launch seam and a random 256 bit-exact vs the oracle."""
+    B = 4096
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+    ra, rb = _gate_dev(ctx, "NAND", host)
+    assert np.array_equal(keyset.decrypt(ra, rb), 1 - (x & y))
+    seams = [0, 1, 1023, 1024, 2047, 2048, 3071, 3072, 4094, 4095]
+    idx = np.unique(np.concatenate([seams, rng.choice(B, 256, replace=False)]))
+    oa, ob = okey.gate_batch("NAND", *(v[idx] for v in host))
+    assert np.array_equal(ra[idx], oa) and np.array_equal(rb[idx], ob)
+
+
+def _bits(wires, x, nb):
+    return dict(zip(wires, T.bits_of(x, nb)))
+
+
+def test_config3_ripple_add_32bit_circuit(ctx, keyset, rng):
+    """configs[2]: one 32-bit ripple-carry addition (depth 32) through the circuit API, plus
+    a few more instances in the same launch sequence, incl. the carry-chain worst cases."""
+    nb = 32
+    C = T.Circuit()
+    a, b = C.inputs(nb), C.inputs(nb)
+    s, co = C.add(a, b)
+    x = np.array([0xFFFFFFFF, 0x89ABCDEF, 1, 0x7FFFFFFF], dtype=np.int64)
+    y = np.array([1, 0x76543211, 0xFFFFFFFF, 0x7FFFFFFF], dtype=np.int64)
+    for B in (1, 4):
+        got = C.run(ctx, B, {**_bits(a, x[:B], nb), **_bits(b, y[:B], nb)}, s + [co], keyset, rng)
+        assert np.array_equal(T.int_of([got[w] for w in s + [co]]), x[:B] + y[:B])
+
+
+def _callers_built():
+    return all(os.path.exists(os.path.join(CALLERS, f)) for f in ("main", "cipher_ops"))
+
+
+def test_config3_cipher_operator_plus_32bit(tmp_path):
+    """configs[2] on the reference's own caller: Cipher::operator+ (Cipher.cpp:348-392, 5 gates
+    per bit through the TFHE C API, one gate at a time) on 32-bit operands, compiled unchanged
+    against libtfhe_amd and run on the MI355X."""
+    if not _callers_built():
+        pytest.skip("oracle/_ref/callers not built (needs the reference sources at build time)")
+    subprocess.run([os.path.join(CALLERS, "main"), "1", "2"], cwd=tmp_path, check=True, timeout=300,
+                   capture_output=True)
+    for av, bv in ((3000000000, 1234567890), (0xFFFFFFFF, 1)):
+        r = subprocess.run([os.path.join(CALLERS, "cipher_ops"), "add32", str(av), str(bv)], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out["a"] == av and out["b"] == bv
+        assert out["sum"] == (av + bv) % 2**32
+        print(f"Cipher::operator+ 32-bit on the MI355X: {out['seconds']:.3f} s")
+
+
+def test_config4_mul_16x16_batch256(ctx, keyset, rng):
+    """configs[3]: 256 independent 16 x 16 -> 32-bit products in one circuit evaluation."""
+    nb, B = 16, 256
+    C = T.Circuit()
+    a, b = C.inputs(nb), C.inputs(nb)
+    p = C.mul(a, b)
+    x = rng.integers(0, 2**nb, B)
+    y = rng.integers(0, 2**nb, B)
+    x[:2] = [2**nb - 1, 0]
+    y[:2] = [2**nb - 1, 2**nb - 1]
+    got = C.run(ctx, B, {**_bits(a, x, nb), **_bits(b, y, nb)}, p, keyset, rng)
+    assert np.array_equal(T.int_of([got[w] for w in p]), x * y)
+
+
+def test_config5_matvec_rows_64x64_16bit(ctx, keyset, rng):
+    """configs[4]: two rows of y = A x for a 64 x 64 16-bit matrix (each row one 64-term dot
+    product circuit; the rows are the circuit's instances, as one rank's shard would be)."""
+    torch = _torch()
+    cols, nbits = 64, 16
+    C, a_w, x_w, y_w = matvec.build(T, cols, nbits)
+    A = rng.integers(0, 2**nbits, (2, cols))
+    A[0] = 2**nbits - 1                              # the largest row sum
+    xv = rng.integers(0, 2**nbits, cols)
+    xv[:8] = 2**nbits - 1
+    y, _ = matvec.run_rows_gpu(T, torch, ctx, keyset, C, a_w, x_w, y_w, A, xv, nbits, rng, reps=1)
+    assert np.array_equal(y, (A.astype(object) @ xv.astype(object)).astype(np.int64))
+
+
+def test_circuit_rows_torus32_vs_oracle(ctx, okey, keyset, rng):
+    """k_blind_rotate_v6_rows + the circuit key switch: each bootstrapped row's output equals
+    the oracle's bootstrap + key switch of the same linear combination, word for word, for
+    MAJ (1, 1, 1), XOR3 (-2, -2, -2) and the 2/1/1 threshold row of the prefix adder."""
+    torch = _torch()
+    C = T.Circuit()
+    x, y, z = C.inputs(3)
+    rows = {"MAJ": (C.gate("MAJ", x, y, z), 0, (1, 1, 1)),
+            "XOR3": (C.gate("XOR3", x, y, z), 0, (-2, -2, -2)),
+            "THRESH_2_1_1": (C.lincomb(E8, 2, x, 1, y, 1, z), E8, (2, 1, 1))}
+    B = 24
+    bits = [rng.integers(0, 2, B) for _ in range(3)]
+    n_w = C.info()["wires"]
+    wa = torch.zeros((n_w, B, n), dtype=torch.int32, device="cuda")
+    wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+    enc = [keyset.encrypt(v, rng) for v in bits]
+    for w, (ea, eb) in zip((x, y, z), enc):
+        wa[w] = torch.from_numpy(ea).cuda()
+        wb[w] = torch.from_numpy(eb).cuda()
+    C.run_dev(ctx, B, wa, wb)
+    torch.cuda.synchronize()
+    ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+    for name, (w, c0, s) in rows.items():
+        la = sum(np.int64(si) * e[0].astype(np.int64) for si, e in zip(s, enc))
+        lb = np.int64(c0) + sum(np.int64(si) * e[1].astype(np.int64) for si, e in zip(s, enc))
+        u_a, u_b = okey.woks_batch(E8, la, lb)
+        oa, ob = okey.keyswitch_batch(u_a, u_b)
+        assert np.array_equal(ha[w], oa) and np.array_equal(hb[w], ob), name
+    ref = C.eval_plain({x: bits[0], y: bits[1], z: bits[2]})
+    for name, (w, _, _) in rows.items():
+        assert np.array_equal(keyset.decrypt(ha[w], hb[w]), ref[w]), name

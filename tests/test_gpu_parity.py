@@ -98,28 +98,6 @@ def test_keyswitch_random_inputs(ctx, okey, rng):
     assert np.array_equal(k_a, o_a) and np.array_equal(k_b, o_b)
 
 
-def test_device_batch_1024_truth_and_sampled_parity(ctx, okey, keyset, rng):
-    """BASELINE config 2: 1024 independent bootsNAND on one GPU; every output decrypts to
-    the truth table, a sample of 32 is checked bit-exactly against the oracle."""
-    torch = _torch()
-    B = 1024
-    x = rng.integers(0, 2, B)
-    y = rng.integers(0, 2, B)
-    a_a, a_b = keyset.encrypt(x, rng)
-    b_a, b_b = keyset.encrypt(y, rng)
-    dev = [torch.from_numpy(v).cuda() for v in (a_a, a_b, b_a, b_b)]
-    r_a = torch.empty((B, n), dtype=torch.int32, device="cuda")
-    r_b = torch.empty(B, dtype=torch.int32, device="cuda")
-    ctx.reserve(B)
-    ctx.gate_dev("NAND", r_a, r_b, *dev)
-    ctx.sync()
-    r_a, r_b = r_a.cpu().numpy(), r_b.cpu().numpy()
-    assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - (x & y))
-    idx = rng.choice(B, 32, replace=False)
-    o_a, o_b = okey.gate_batch("NAND", a_a[idx], a_b[idx], b_a[idx], b_b[idx])
-    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
-
-
 def test_kernel_generations_agree(ctx, keyset, rng):
     """Every blind-rotation generation (v1 LDS radix-2, v2, v3, v4, v5 exact NTT; v6, v7 fp64
     FFT, whose rounded products equal the exact ones) gives identical Torus32 results on the
