@@ -189,12 +189,29 @@ __device__ __forceinline__ void br_v4_body(V4Shared &sh, const V4Args &g, const 
     if (tid == 0) *ub = (int32_t)sh.E[1][0];
 }
 
+// Guard mode (engine.h Guard): the fp64 kernel ran first and flagged each ciphertext with its
+// largest rounding distance; a ciphertext under the threshold keeps its result (the workgroup
+// exits before touching anything), one at or above it is recomputed here exactly.
+struct V4Guard {
+    const uint32_t *flags;   // null: not in guard mode
+    uint32_t hi;             // threshold (high word of the distance)
+    uint32_t *stats;         // [0]: recomputed ciphertexts
+};
+__device__ __forceinline__ bool guard_skip(const V4Guard &gd, size_t slot) {
+    if (!gd.flags) return false;
+    const uint32_t f0 = gd.flags[2 * slot], f1 = gd.flags[2 * slot + 1];
+    if ((f0 > f1 ? f0 : f1) < gd.hi) return true;   // uniform over the workgroup
+    if (threadIdx.x == 0) atomicAdd(gd.stats, 1u);
+    return false;
+}
+
 // gate batch: ciphertext gct of half h = gct / B reads in_h at index gct mod B
 __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int B, BrInput in0, BrInput in1,
                                                                 int32_t mu, int32_t *__restrict__ u_a,
-                                                                int32_t *__restrict__ u_b) {
+                                                                int32_t *__restrict__ u_b, V4Guard gd) {
     __shared__ V4Shared sh;
     const int gct = blockIdx.x;
+    if (guard_skip(gd, (size_t)gct)) return;
     const int half = gct >= B;
     const int idx = half ? gct - B : gct;
     const BrInput &in = half ? in1 : in0;
@@ -212,9 +229,11 @@ __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_rows(V4Args g
                                                                      const int32_t *__restrict__ wa,
                                                                      const int32_t *__restrict__ wb, int32_t mu,
                                                                      int32_t *__restrict__ u_a,
-                                                                     int32_t *__restrict__ u_b) {
+                                                                     int32_t *__restrict__ u_b, int row0,
+                                                                     V4Guard gd) {
     __shared__ V4Shared sh;
-    const int k = blockIdx.x, r = blockIdx.y;
+    const int k = blockIdx.x, r = row0 + (int)blockIdx.y;
+    if (guard_skip(gd, (size_t)r * B + k)) return;
     const CircRow row = rows[r];
     auto wire = [&](int w, const int32_t *&pa, const int32_t *&pb) {
         if (w < 0) { pa = nullptr; pb = nullptr; return; }
@@ -300,21 +319,32 @@ static V4Args v4_args(const DeviceKey &key) {
     return g;
 }
 
+static V4Guard v4_guard(const Guard *guard) {
+    V4Guard gd{nullptr, 0u, nullptr};
+    if (guard && guard->flags) gd = V4Guard{guard->flags, guard_threshold_hi(), guard->stats};
+    return gd;
+}
+
 hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s) {
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard) {
     if (B <= 0) return hipSuccess;
+    if (!key.bk_v2) return hipErrorInvalidValue;
     const BrInput in1 = halves > 1 ? in[1] : in[0];
     hipLaunchKernelGGL(k_blind_rotate_v4, dim3(B * halves), dim3(kV4Threads), 0, s, v4_args(key), B, in[0], in1, mu,
-                       u_a, u_b);
+                       u_a, u_b, v4_guard(guard));
     return hipGetLastError();
 }
 
 hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                       const Guard *guard) {
     if (B <= 0 || nrows <= 0) return hipSuccess;
-    if (nrows > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_v4_rows, dim3(B, nrows), dim3(kV4Threads), 0, s, v4_args(key), B, rows, wa, wb,
-                       mu, u_a, u_b);
+    if (!key.bk_v2) return hipErrorInvalidValue;
+    for (int r0 = 0; r0 < nrows; r0 += 65535) {   // grid y is limited to 65535 rows per launch
+        const int n = nrows - r0 < 65535 ? nrows - r0 : 65535;
+        hipLaunchKernelGGL(k_blind_rotate_v4_rows, dim3(B, n), dim3(kV4Threads), 0, s, v4_args(key), B, rows, wa, wb,
+                           mu, u_a, u_b, r0, v4_guard(guard));
+    }
     return hipGetLastError();
 }
 

@@ -102,6 +102,8 @@ static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave bu
 
 struct V6Args {
     const double2 *bk;   // [kn][4 rows][2 c][8 r][64 L]: FFT-domain key / 512, slot 8 L + r
+    uint32_t *flags;     // exactness guard (engine.h Guard): [2 slot + w] max rounding distance, or null
+    uint32_t *stats;     // [1]: the largest distance (high word) seen
     const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
     int prio;            // issue-priority policy, see set_prio_level
     int prio_shift;      // policies 2, 5: steps per level = 2^prio_shift
@@ -134,7 +136,7 @@ __device__ __forceinline__ void set_prio_level(unsigned lvl) {
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
 template <int WAVES>
 __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int L,
-                                        uint32_t (&acc)[16] V6_STAMPS_PARAM) {
+                                        uint32_t (&acc)[16], double &mx V6_STAMPS_PARAM) {
     double2 *X = sh.X[w];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
@@ -232,11 +234,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
         }
     }
     V6_STAMP(7);
-    // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im)
+    // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im); mx tracks the
+    // rounding distance for the exactness guard
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        acc[r] += torus_of(Y[r].re);
-        acc[r + 8] += torus_of(Y[r].im);
+        acc[r] += torus_of_chk(Y[r].re, mx);
+        acc[r + 8] += torus_of_chk(Y[r].im, mx);
     }
     wave_sync();
     V6_STAMP(8);
@@ -244,7 +247,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
 
 template <int WAVES>
 __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const RowTerms6 &t, int32_t mu,
-                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub) {
+                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot) {
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
@@ -286,6 +289,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     stamps.prev = __builtin_amdgcn_s_memtime();
 #endif
     const int prio = g.prio;
+    double mx = 0.0;                     // largest rounding distance of this lane (guard)
     int a_next = sh.bara[0];
     for (int i = 0; i < kn; ++i) {
         const int a = a_next;
@@ -300,7 +304,14 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc V6_STAMPS_ARG);
+        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc, mx V6_STAMPS_ARG);
+    }
+    if (g.flags) {   // exactness guard: this wave's largest rounding distance (high word)
+        const uint32_t h = wave_max_hi(mx);
+        if (L == 0) {
+            g.flags[2 * slot + w] = h;
+            atomicMax(g.stats + 1, h);
+        }
     }
 #ifdef TFHE_AMD_V6_STAMPS
     if (blockIdx.x == 0 && blockIdx.y == 0 && L == 0)
@@ -341,7 +352,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g,
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES>(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+    br_v6_body<WAVES>(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
 }
 
 template <int WAVES>
@@ -367,7 +378,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Ar
     wire(row.y, t.ya, t.yb);
     wire(row.z, t.za, t.zb);
     const size_t slot = (size_t)r * B + k;
-    br_v6_body<WAVES>(sh, g, t, mu, u_a + slot * kN, u_b + slot);
+    br_v6_body<WAVES>(sh, g, t, mu, u_a + slot * kN, u_b + slot, slot);
 }
 
 __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
@@ -390,7 +401,8 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #ifdef TFHE_AMD_V6_STAMPS
         V6Stamps stamps;
 #endif
-        cmux_v6<2>(sh, g, tA, i, a, w, L, ac V6_STAMPS_ARG);
+        double mx = 0.0;
+        cmux_v6<2>(sh, g, tA, i, a, w, L, ac, mx V6_STAMPS_ARG);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];
@@ -498,9 +510,11 @@ static int v6_prio_policy(const DeviceKey &key, long wgs) {
     return wgs > 4L * v6_cus(key) ? 1 : 5;
 }
 
-static V6Args v6_args(const DeviceKey &key, long wgs) {
+static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullptr) {
     V6Args g;
     g.bk = key.bk_fft;
+    g.flags = guard ? guard->flags : nullptr;
+    g.stats = guard ? guard->stats : nullptr;
     g.tw = key.tw6;
     g.prio = wgs > 0 ? v6_prio_policy(key, wgs) : 0;
     static const char *sh = getenv("TFHE_AMD_PRIO_S");
@@ -510,21 +524,22 @@ static V6Args v6_args(const DeviceKey &key, long wgs) {
 }
 
 hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s) {
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard) {
     if (B <= 0) return hipSuccess;
     if (!key.bk_fft) return hipErrorInvalidValue;
     const BrInput in1 = halves > 1 ? in[1] : in[0];
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s, v6_args(key, n), B,
-                           (int)base, in[0], in1, mu, u_a, u_b);
+        hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                           v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                       const Guard *guard) {
     if (B <= 0 || nrows <= 0) return hipSuccess;
     if (!key.bk_fft) return hipErrorInvalidValue;
     const long total = (long)B * nrows, chunk = v6_chunk(key);
@@ -532,7 +547,7 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
         const long n = total - base < chunk ? total - base : chunk;
         if (n > 0x7fffffffL) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_blind_rotate_v6_rows<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                           v6_args(key, n), B, base, rows, wa, wb, mu, u_a, u_b);
+                           v6_args(key, n, guard), B, base, rows, wa, wb, mu, u_a, u_b);
     }
     return hipGetLastError();
 }

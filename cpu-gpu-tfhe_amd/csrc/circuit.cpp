@@ -58,6 +58,7 @@ struct TfheAmdCircuit {
     int dev = -1;
     void *d_tab = nullptr;
     int32_t *u_a = nullptr, *u_b = nullptr;
+    uint32_t *u_flags = nullptr;   // exactness-guard flags, 2 words per u slot (engine.h Guard)
     size_t u_slots = 0;
     StreamFence fence;   // u scratch reuse across caller streams
     ~TfheAmdCircuit() { release(); }
@@ -70,7 +71,8 @@ struct TfheAmdCircuit {
         if (d_tab) (void)hipFree(d_tab);
         if (u_a) (void)hipFree(u_a);
         if (u_b) (void)hipFree(u_b);
-        d_tab = nullptr; u_a = nullptr; u_b = nullptr; u_slots = 0; dev = -1;
+        if (u_flags) (void)hipFree(u_flags);
+        d_tab = nullptr; u_a = nullptr; u_b = nullptr; u_flags = nullptr; u_slots = 0; dev = -1;
     }
 };
 
@@ -303,7 +305,7 @@ extern "C" int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_lev
 
 // wires_a [n_wires][B][500], wires_b [n_wires][B] on the context's device; input wires filled
 int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
-                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb) {
+                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb, uint32_t *guard_stats) {
     if (!c->compiled) {
         const int rc = compile(c);
         if (rc != TFHE_AMD_OK) return rc;
@@ -330,9 +332,11 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
         (void)hipDeviceSynchronize();   // the old scratch may still be in use
         if (c->u_a) (void)hipFree(c->u_a);
         if (c->u_b) (void)hipFree(c->u_b);
-        c->u_a = nullptr; c->u_b = nullptr; c->u_slots = 0;
+        if (c->u_flags) (void)hipFree(c->u_flags);
+        c->u_a = nullptr; c->u_b = nullptr; c->u_flags = nullptr; c->u_slots = 0;
         if (hipMalloc(&c->u_a, sizeof(int32_t) * kN * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
         if (hipMalloc(&c->u_b, sizeof(int32_t) * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        if (hipMalloc(&c->u_flags, sizeof(uint32_t) * 2 * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
         c->u_slots = need;
     }
     if (c->fence.acquire(s) != hipSuccess) return TFHE_AMD_E_HIP;
@@ -341,8 +345,9 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
     const CircLin *d_lin = (const CircLin *)(d_ks + c->ks.size());
     for (const auto &lv : c->levels) {
         if (lv.nrows) {
+            const Guard gd = guard_stats ? Guard{c->u_flags, guard_stats} : Guard{};
             const hipError_t e =
-                launch_blind_rotate_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s);
+                launch_blind_rotate_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s, &gd);
             if (e != hipSuccess) return TFHE_AMD_E_HIP;
             if (launch_keyswitch_rows(key, B, lv.nks, d_ks + lv.ks0, c->u_a, c->u_b, wa, wb, s) != hipSuccess)
                 return TFHE_AMD_E_HIP;

@@ -82,27 +82,45 @@ int br_version() {
     return v;
 }
 
+// high word of the rounding distance at which the exact kernel recomputes a ciphertext: 1/4
+// (0x3FD00000) by default; tfhe_amd_set_guard_threshold changes it (tests force the fallback with
+// 0; values >= 1/2 can never trigger, the distance being <= 1/2)
+static std::atomic<uint32_t> g_guard_hi{0x3FD00000u};
+uint32_t guard_threshold_hi() { return g_guard_hi.load(std::memory_order_relaxed); }
+
+// the default fp64 kernel, then the exact kernel in guard mode over the flags it wrote
+static hipError_t run_v6_guarded(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
+                                 int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard) {
+    hipError_t e = launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s, guard);
+    if (e != hipSuccess || !guard || !guard->flags) return e;
+    return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s, guard);
+}
+
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
-                         int32_t *u_b, hipStream_t s) {
+                         int32_t *u_b, hipStream_t s, const Guard *guard) {
     switch (br_version()) {
     case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
     case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
     case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
     case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
-    case 6: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
     case 7: return launch_blind_rotate_v7(key, B, halves, in, mu, u_a, u_b, s);
-    default: return launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s);
+    default: return run_v6_guarded(key, B, halves, in, mu, u_a, u_b, s, guard);   // 0, 6
     }
 }
 
 hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s) {
+                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                    const Guard *guard) {
     switch (br_version()) {
     case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     case 7: return launch_blind_rotate_v7_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
-    default: return launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+    default: {
+        hipError_t e = launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
+        if (e != hipSuccess || !guard || !guard->flags) return e;
+        return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
+    }
     }
 }
 
@@ -121,6 +139,8 @@ struct TfheAmdContext {
     int32_t *u_a = nullptr;   // [2 cap][kN]   extracted samples (2 halves for MUX)
     int32_t *u_b = nullptr;   // [2 cap]
     int32_t *io = nullptr;    // host-API staging: inputs 3 x (cap x 501) + outputs cap x 501
+    uint32_t *gflags = nullptr;   // exactness guard flags: 2 words per ciphertext (2 cap ciphertexts)
+    uint32_t *gstats = nullptr;   // guard counters (engine.h Guard), zeroed at creation
     // pinned host staging for the host API
     int32_t *h_io = nullptr;
     // profiling
@@ -167,7 +187,9 @@ static int free_scratch(TfheAmdContext *c) {
     if (c->u_b) (void)hipFree(c->u_b);
     if (c->io) (void)hipFree(c->io);
     if (c->h_io) (void)hipHostFree(c->h_io);
+    if (c->gflags) (void)hipFree(c->gflags);
     c->u_a = c->u_b = c->io = c->h_io = nullptr;
+    c->gflags = nullptr;
     c->cap = 0;
     return 0;
 }
@@ -185,6 +207,7 @@ int tfhe_amd_reserve(TfheAmdContext *c, int B) {
     HIPCHK(hipMalloc(&c->u_a, sizeof(int32_t) * 2 * (size_t)cap * kN));
     HIPCHK(hipMalloc(&c->u_b, sizeof(int32_t) * 2 * (size_t)cap));
     HIPCHK(hipMalloc(&c->io, sizeof(int32_t) * io_words(cap)));
+    HIPCHK(hipMalloc(&c->gflags, sizeof(uint32_t) * 4 * (size_t)cap));
     HIPCHK(hipHostMalloc(&c->h_io, sizeof(int32_t) * io_words(cap), hipHostMallocDefault));
     c->cap = cap;
     return TFHE_AMD_OK;
@@ -199,6 +222,8 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
     c->key.device = device;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->gstats, sizeof(uint32_t) * 4));
+    HIPCHK(hipMemset(c->gstats, 0, sizeof(uint32_t) * 4));
 
     NttTables *ht = new NttTables;
     build_ntt_tables(ht);
@@ -285,6 +310,7 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     if (c->copy_in) (void)hipStreamDestroy(c->copy_in);
     if (c->copy_out) (void)hipStreamDestroy(c->copy_out);
     free_scratch(c);
+    if (c->gstats) (void)hipFree(c->gstats);
     if (!c->shared_key) free_key(c->key);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -382,6 +408,18 @@ static bool gate_spec(int gate, int32_t *c, int32_t *sa, int32_t *sb) {
 
 static const int32_t kMu = 1 << 29;   // modSwitchToTorus32(1, 8)
 
+// TFHE_AMD_GUARD=0 turns the guard off (A/B timing only: no flags, no exact-kernel launch)
+static bool guard_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("TFHE_AMD_GUARD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+static Guard ctx_guard(TfheAmdContext *c) {
+    return c->gflags && c->gstats && guard_enabled() ? Guard{c->gflags, c->gstats} : Guard{};
+}
+
 extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                        const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
                                        const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b,
@@ -401,7 +439,8 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
         BrInput in[2] = {{ca_a, ca_b, cb_a, cb_b, -kMu, 1, 1}, {ca_a, ca_b, cc_a, cc_b, -kMu, -1, 1}};
         {
             ProfScope ps(c, s, true);
-            HIPCHK(run_br(c->key, B, 2, in, kMu, c->u_a, c->u_b, s));
+            const Guard gd = ctx_guard(c);
+            HIPCHK(run_br(c->key, B, 2, in, kMu, c->u_a, c->u_b, s, &gd));
         }
         ProfScope ps(c, s, false);
         HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, c->u_a + (size_t)B * kN, c->u_b + B, kMu,
@@ -414,7 +453,8 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     in.x_a = ca_a; in.x_b = ca_b; in.y_a = cb_a; in.y_b = cb_b;
     {
         ProfScope ps(c, s, true);
-        HIPCHK(run_br(c->key, B, 1, &in, kMu, c->u_a, c->u_b, s));
+        const Guard gd = ctx_guard(c);
+        HIPCHK(run_br(c->key, B, 1, &in, kMu, c->u_a, c->u_b, s, &gd));
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
@@ -429,9 +469,16 @@ extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32
     if (!x_a || !x_b || !u_a || !u_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    int rc = tfhe_amd_reserve(c, B);   // guard flags live in the context's scratch
+    if (rc) return rc;
+    HIPCHK(c->fence.acquire(s));
     BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
-    ProfScope ps(c, s, true);
-    HIPCHK(run_br(c->key, B, 1, &in, mu, u_a, u_b, s));
+    {
+        ProfScope ps(c, s, true);
+        const Guard gd = ctx_guard(c);
+        HIPCHK(run_br(c->key, B, 1, &in, mu, u_a, u_b, s, &gd));
+    }
+    HIPCHK(c->fence.done(s));
     return TFHE_AMD_OK;
 }
 
@@ -448,7 +495,8 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     BrInput in{x_a, x_b, nullptr, nullptr, 0, 1, 0};
     {
         ProfScope ps(c, s, true);
-        HIPCHK(run_br(c->key, B, 1, &in, mu, c->u_a, c->u_b, s));
+        const Guard gd = ctx_guard(c);
+        HIPCHK(run_br(c->key, B, 1, &in, mu, c->u_a, c->u_b, s, &gd));
     }
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, c->u_a, c->u_b, nullptr, nullptr, 0, res_a, res_b, s));
@@ -558,13 +606,26 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
     const bool mux = gate == TFHE_GATE_MUX;
     if (mux && (!cc_a || !cc_b)) return TFHE_AMD_E_ARG;
+    {   // refuse an unknown gate before anything is staged or enqueued
+        int32_t k0, k1, k2;
+        if (!mux && !gate_spec(gate, &k0, &k1, &k2)) return TFHE_AMD_E_ARG;
+    }
+    if (!c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
     if (host_slice() > 0 && B > host_slice()) {
         const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
-        return gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);
+        rc = gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);
+        if (rc) {
+            // copies of earlier slices may still be in flight on the copy streams, not ordered
+            // against the next call's staging on c->stream: drain everything before returning
+            if (c->copy_in) (void)hipStreamSynchronize(c->copy_in);
+            (void)hipStreamSynchronize(c->stream);
+            if (c->copy_out) (void)hipStreamSynchronize(c->copy_out);
+        }
+        return rc;
     }
     const size_t A = (size_t)B * kn;
     // staging layout: [ca_a | cb_a | cc_a | res_a] then [ca_b | cb_b | cc_b | res_b]
@@ -644,6 +705,8 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
     c->shared_key = true;
     if (hipSetDevice(c->device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->gstats, sizeof(uint32_t) * 4) != hipSuccess ||
+        hipMemset(c->gstats, 0, sizeof(uint32_t) * 4) != hipSuccess ||
         tfhe_amd_reserve(c, 64) != TFHE_AMD_OK) {
         tfhe_amd_context_destroy(c);
         return nullptr;
@@ -653,7 +716,7 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
 
 // circuit.cpp
 int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
-                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb);
+                                  TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb, uint32_t *guard_stats);
 
 extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ, int B, int32_t *wires_a,
                                         int32_t *wires_b, void *stream) {
@@ -663,7 +726,32 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
     std::lock_guard<std::mutex> lk(c->mu);
-    return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b);
+    return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b, c->gstats);
+}
+
+extern "C" int tfhe_amd_set_guard_threshold(double distance) {
+    if (!(distance >= 0.0)) return TFHE_AMD_E_ARG;
+    uint64_t bits;
+    memcpy(&bits, &distance, 8);
+    g_guard_hi.store((uint32_t)(bits >> 32));
+    return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_guard_stats(TfheAmdContext *c, double *max_distance, long long *recomputed, int reset) {
+    if (!c || !c->gstats) return TFHE_AMD_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());   // launches on caller streams update the counters
+    uint32_t h[4];
+    HIPCHK(hipMemcpy(h, c->gstats, sizeof h, hipMemcpyDeviceToHost));
+    if (max_distance) {
+        const uint64_t bits = (uint64_t)h[1] << 32;   // high word: the distance rounded down
+        double d;
+        memcpy(&d, &bits, 8);
+        *max_distance = d;
+    }
+    if (recomputed) *recomputed = h[0];
+    if (reset) HIPCHK(hipMemset(c->gstats, 0, sizeof h));
+    return TFHE_AMD_OK;
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {

@@ -74,6 +74,19 @@ struct StreamFence {
     }
 };
 
+// Exactness guard of the fp64 FFT blind rotation.  The v6 kernel rounds each
+// external-product coefficient c to the nearest integer; that equals the exact product while the
+// FFT error stays below 1/2.  Every wave tracks the largest rounding distance |c - rint(c)| it
+// sees over all 500 steps and stores its high word (monotone in the distance) in flags[2 slot + w];
+// an exact-NTT (v4) launch in guard mode then recomputes every ciphertext whose flag reaches the
+// threshold (1/4 by default) and exits at once for all others.  stats[0] counts the recomputed
+// ciphertexts, stats[1] holds the largest high word seen (tfhe_amd_guard_stats).
+struct Guard {
+    uint32_t *flags = nullptr;
+    uint32_t *stats = nullptr;
+};
+uint32_t guard_threshold_hi();
+
 // BK conversion (coefficient -> NTT domain) on the device; d_bk_coef = [kn][4][2][kN]
 hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const NttTables *d_tab,
                             hipStream_t s);
@@ -97,13 +110,15 @@ hipError_t launch_blind_rotate_v3_debug(const DeviceKey &key, int B, int iters, 
                                         const int32_t *bara, hipStream_t s);
 // v4 (v2 layout, inverse CT + lazy CRT + periodic accumulator), blind_rotate_v4.hip
 void build_v4_twiddles(const NttTables &t, uint2 *tu_i, uint2 *ts_i, uint2 *tpost);
+// guard != null: guard mode (recompute only the ciphertexts whose v6 flag reached the threshold)
 hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
 // circuit level (v4 kernel): B instances x nrows rows, wires [W][B] ciphertexts, u slots r B + k
 hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                       const Guard *guard = nullptr);
 // v5 (latency: 8 waves per ciphertext), blind_rotate_v5.hip; same results as v4
 hipError_t launch_blind_rotate_v5(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                   int32_t *u_a, int32_t *u_b, hipStream_t s);
@@ -112,10 +127,12 @@ hipError_t launch_blind_rotate_v5_rows(const DeviceKey &key, int B, int nrows, c
 // v6 (fp64 FFT external product, the reference's arithmetic), blind_rotate_v6.hip
 void build_v6_twiddles(double2 *tw);
 hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s);
+// guard != null: write the rounding-distance flags (Guard) for the guard launch that follows
 hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
+                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                       const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
 // v7 (v6 arithmetic; BK_i staged in LDS by LDS-DMA and shared by the workgroup's ciphertexts),
@@ -128,9 +145,11 @@ hipError_t launch_blind_rotate_v7_debug(const DeviceKey &key, int B, int iters, 
                                         const int32_t *bara, hipStream_t s);
 // which blind-rotation kernel runs: 0 = default (v6), 1..7 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
-// circuit level blind rotation with the selected kernel (rows variants of v4 / v5 / v6)
+// circuit level blind rotation with the selected kernel (rows variants of v4 / v5 / v6); the
+// default fp64 kernel runs guarded (flags: 2 words per row x instance)
 hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
+                                    const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
+                                    const Guard *guard);
 
 // which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)
 int ks_version();

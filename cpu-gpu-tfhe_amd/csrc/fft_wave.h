@@ -272,6 +272,32 @@ __device__ __forceinline__ uint32_t torus_of(double c) {
     return (uint32_t)__double_as_longlong(y);
 }
 
+// the same, and mx = max(mx, |c - rint(c)|): q = t + y = k + rint(c - k) is exact (|c| < 2^52),
+// and so is c - q (Fast2Sum error of y; Sterbenz) — the exactness guard's measurement, 2 fp64
+// adds and one max per coefficient (TFHE_AMD_V6_NOGUARD: A/B builds without it)
+__device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx) {
+    constexpr double M1 = 0x1.8p84, M12 = 0x1.8p84 + 0x1.8p52;
+    const double s = c + M1;
+    const double t = s - M12;
+    const double y = c - t;
+#ifndef TFHE_AMD_V6_NOGUARD
+    const double q = t + y;
+    mx = __builtin_fmax(mx, __builtin_fabs(c - q));
+#endif
+    return (uint32_t)__double_as_longlong(y);
+}
+
+// high word of a non-negative double: monotone in its value, max-reduced across the wave
+__device__ __forceinline__ uint32_t wave_max_hi(double v) {
+    uint32_t h = (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)h, off, 64);
+        h = o > h ? o : h;
+    }
+    return h;
+}
+
 __device__ __forceinline__ void e6_store(uint32_t *E, int j, uint32_t v, bool third) {
     E[j] = v;
     E[j + kN] = 0u - v;

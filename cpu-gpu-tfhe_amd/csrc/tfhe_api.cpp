@@ -23,6 +23,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <algorithm>
 #include <mutex>
 #include <random>
 #include <unordered_map>
@@ -573,18 +574,55 @@ static void forget_device_keys(const void *k1, const void *k2) {
     }
 }
 
-// this thread's lane (own stream + scratch) on the key's device
+// This thread's lanes (own stream + scratch) on each key's device.  A thread that exits gives
+// its lanes back (the holder's destructor), so callers that spawn short-lived threads (a
+// std::thread per request, non-pooled OpenMP teams) do not accumulate streams, scratch and
+// pinned memory per thread; a key deleted first has already destroyed its lanes (the weak
+// reference is then expired, or the lane is no longer listed).
+struct LaneHolder {
+    struct Slot {
+        std::weak_ptr<KeyEntry> entry;
+        TfheAmdContext *lane;
+    };
+    std::unordered_map<uint64_t, Slot> slots;
+    ~LaneHolder() {
+        for (auto &kv : slots) {
+            std::shared_ptr<KeyEntry> e = kv.second.entry.lock();
+            if (!e) continue;
+            std::lock_guard<std::mutex> lk(e->mu);
+            auto it = std::find(e->lanes.begin(), e->lanes.end(), kv.second.lane);
+            if (it == e->lanes.end()) continue;
+            e->lanes.erase(it);
+            tfhe_amd_context_destroy(kv.second.lane);
+        }
+    }
+};
+
 static TfheAmdContext *lane_for(const LweBootstrappingKeyFFT *bkfft, const LweKeySwitchKey *ks) {
-    thread_local std::unordered_map<uint64_t, TfheAmdContext *> lanes;
+    thread_local LaneHolder holder;
     std::shared_ptr<KeyEntry> e = entry_for(bkfft, ks);
-    auto it = lanes.find(e->id);
-    if (it != lanes.end()) return it->second;
+    auto it = holder.slots.find(e->id);
+    if (it != holder.slots.end()) return it->second.lane;
     std::lock_guard<std::mutex> lk(e->mu);
     TfheAmdContext *l = tfhe_amd_context_lane(e->primary);
     if (!l) die_dramatically("tfhe_amd: cannot create a per-thread GPU lane");
     e->lanes.push_back(l);
-    lanes[e->id] = l;
+    holder.slots[e->id] = LaneHolder::Slot{e, l};
     return l;
+}
+
+// lanes currently alive for the Tier-1 key of `bk` (tests: threads give their lanes back)
+EXPORT int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk) {
+    if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
+    std::shared_ptr<KeyEntry> e;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find(bk->bkFFT);
+        if (it == g_reg.end()) return 0;
+        e = it->second;
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    return (int)e->lanes.size();
 }
 
 EXPORT int tfhe_amd_set_default_device(int device) {

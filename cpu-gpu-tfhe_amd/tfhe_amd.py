@@ -72,6 +72,10 @@ def _load():
     L.tfhe_amd_profile_enable.argtypes = [_VP, ctypes.c_int]
     L.tfhe_amd_profile_read.argtypes = [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    L.tfhe_amd_guard_stats.argtypes = [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                                       ctypes.c_int]
+    L.tfhe_amd_set_guard_threshold.argtypes = [ctypes.c_double]
+    L.tfhe_amd_tier1_lane_count.argtypes = [_VP]
     L.tfhe_random_generator_setSeed.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.modSwitchToTorus32.restype = ctypes.c_int32
     L.modSwitchFromTorus32.restype = ctypes.c_int
@@ -103,6 +107,12 @@ def version():
 def select_kernel(generation):
     """tfhe_amd_select_kernel: blind-rotation kernel generation 1..7 (A/B and cross-checks; 0 = default)."""
     _check(lib.tfhe_amd_select_kernel(int(generation)), "select_kernel")
+
+
+def set_guard_threshold(distance):
+    """tfhe_amd_set_guard_threshold: rounding distance at which the fp64 kernel's results are
+    recomputed by the exact NTT kernel (default 1/4; 0 recomputes everything)."""
+    _check(lib.tfhe_amd_set_guard_threshold(float(distance)), "set_guard_threshold")
 
 
 def _p(a):
@@ -359,15 +369,17 @@ class Context:
         return r_a, r_b
 
     # ---- device (torch) batches: tensors must be int32 CUDA/HIP tensors, contiguous
-    @staticmethod
-    def _dev_check(t, shape, name):
-        """The kernels index by shape: refuse anything that would make them read or write out
-        of bounds before it reaches the GPU."""
+    def _dev_check(self, t, shape, name):
+        """The kernels index by shape and run on this context's GPU: refuse anything that would
+        make them read or write out of bounds, or touch another device's memory, before it
+        reaches the GPU."""
         if t is None:
             raise TfheAmdError(f"{name}: missing tensor")
         if not t.is_cuda or t.dtype != torch.int32 or not t.is_contiguous() or tuple(t.shape) != shape:
             raise TfheAmdError(f"{name}: need a contiguous int32 GPU tensor of shape {shape}, got "
                                f"{tuple(t.shape)} {t.dtype} cuda={t.is_cuda} contiguous={t.is_contiguous()}")
+        if t.device.index is not None and t.device.index != self.device:
+            raise TfheAmdError(f"{name}: tensor is on cuda:{t.device.index}, the context on cuda:{self.device}")
 
     def gate_dev(self, gate, res_a, res_b, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, stream=None):
         g = GATES[gate] if isinstance(gate, str) else int(gate)
@@ -391,6 +403,13 @@ class Context:
         _check(lib.tfhe_amd_blind_rotate_dev(self.h, B, int(iters), acc.data_ptr(),
                                              None if bara is None else bara.data_ptr(), stream),
                "blind_rotate_dev")
+
+    def guard_stats(self, reset=False):
+        """(largest rounding distance measured, ciphertexts recomputed exactly) since the last
+        reset (tfhe_amd_guard_stats; synchronizes the device)."""
+        d = ctypes.c_double(); r = ctypes.c_longlong()
+        _check(lib.tfhe_amd_guard_stats(self.h, ctypes.byref(d), ctypes.byref(r), int(bool(reset))), "guard_stats")
+        return d.value, r.value
 
     def profile_enable(self, on=True):
         _check(lib.tfhe_amd_profile_enable(self.h, int(on)), "profile_enable")

@@ -121,6 +121,10 @@ int tfhe_amd_profile_read(TfheAmdContext *ctx, double *br_ms, int *br_launches,
 int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
                          const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk);
 
+/* Number of per-thread lanes (stream + scratch) the Tier-1 API holds for this cloud key;
+ * a thread's lanes are released when it exits (0 if the key has no device context). */
+int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
+
 /* Device selection for the Tier-1 (single-gate) API: the GPU used by the cached
  * context of every cloud key (default 0). */
 int tfhe_amd_set_default_device(int device);
@@ -141,6 +145,17 @@ int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32
  * env TFHE_AMD_BR=<n> does the same at startup.  For A/B measurements and parity
  * cross-checks; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
+
+/* Exactness guard of the default fp64 FFT blind rotation: every launch
+ * measures, per ciphertext, the largest distance |c - rint(c)| of any rounded external-product
+ * coefficient over its 500 steps; a ciphertext at or above the threshold (default 1/4; the
+ * result is exact while the FFT error stays below 1/2) is recomputed by the exact 2-prime NTT
+ * kernel in the same stream before its key switch.  guard_stats reads (and optionally resets)
+ * the context's largest measured distance and its count of recomputed ciphertexts (it
+ * synchronizes the device).  set_guard_threshold is process-wide (0 recomputes everything:
+ * tests). */
+int tfhe_amd_guard_stats(TfheAmdContext *ctx, double *max_distance, long long *recomputed, int reset);
+int tfhe_amd_set_guard_threshold(double distance);
 
 /* build tag, e.g. "tfhe_amd gfx950 fft64 br-v6 ks-v4" */
 const char *tfhe_amd_version(void);

@@ -5,15 +5,18 @@ set -u
 mkdir -p gpurun_out
 for rep in $(seq 1 ${AB_REPS:-1}); do
 for n in "$@"; do
-  # "base" = lib/ (default kernel), "brN" = lib/ with TFHE_AMD_BR=N, else variants/<name>/
-  br=0
+  # "base" = lib/ (default kernel), "brN" = lib/ with TFHE_AMD_BR=N, "noguard" = lib/ with
+  # TFHE_AMD_GUARD=0, "<variant>-ng" = variants/<variant>/ with TFHE_AMD_GUARD=0, else variants/<name>/
+  br=0; guard=1
   case "$n" in
     base) lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so ;;
+    noguard) lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so; guard=0 ;;
+    *-ng) lib=cpu-gpu-tfhe_amd/variants/${n%-ng}/libtfhe_amd.so; guard=0 ;;
     br*) lib=cpu-gpu-tfhe_amd/lib/libtfhe_amd.so; br=${n#br} ;;
     *) lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so ;;
   esac
   log=gpurun_out/ab_${n}_${AB_BATCH:-1024}_$rep.log
-  TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline > $log 2>&1
+  TFHE_AMD_GUARD=$guard TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline --no-clock --extra-batches '' --strong-batch 0 > $log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; tail -5 $log; exit $rc; }
   python3 -c "
 import json,sys

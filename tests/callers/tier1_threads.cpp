@@ -5,6 +5,8 @@
 // Every gate of the API is evaluated on the same encrypted inputs three ways — sequentially,
 // from 8 OpenMP threads at once, and in place — and the three results must be the same
 // samples, word for word (the engine is deterministic); each must decrypt to its truth table.
+// Then 16 short-lived std::threads each run one gate and exit: every exiting thread must give
+// its lane (stream + scratch) back, so the key's lane count returns to what it was.
 // Prints one JSON line; exit status 0 only when everything matched.
 #include <cstdio>
 #include <cstdint>
@@ -12,7 +14,9 @@
 #include <cstring>
 #include <vector>
 #include <omp.h>
+#include <thread>
 #include "tfhe/tfhe.h"
+#include "tfhe_amd.h"
 
 typedef void (*Gate2)(LweSample *, const LweSample *, const LweSample *, const TFheGateBootstrappingCloudKeySet *);
 
@@ -95,6 +99,18 @@ int main(int argc, char **argv) {
             bootsMUX(r, &a[i], &b[i], r, bk);
         }
     }
+    // short-lived threads: one gate each, then exit
+    const int lanes_before = tfhe_amd_tier1_lane_count(bk);
+    int short_errors = 0;
+    for (int t = 0; t < 16; t++) {
+        LweSample *r = new_gate_bootstrapping_ciphertext_array(1, params);
+        const int i = t % n;
+        std::thread th([&] { bootsNAND(r, &a[i], &b[i], bk); });
+        th.join();
+        short_errors += !same(r, &seq[i], dim);   // gate 0 is NAND: seq[i] = NAND(a[i], b[i])
+        delete_gate_bootstrapping_ciphertext_array(1, r);
+    }
+    const int lanes_after = tfhe_amd_tier1_lane_count(bk);
     int par_mismatch = 0, alias_mismatch = 0, truth_errors = 0;
     for (int k = 0; k < total; k++) {
         const int g = k / n, i = k % n;
@@ -104,8 +120,10 @@ int main(int argc, char **argv) {
         truth_errors += bootsSymDecrypt(&seq[k], key) != want;
     }
     printf("{\"units\": %d, \"per_unit\": %d, \"threads\": 8, \"par_mismatch\": %d, \"alias_mismatch\": %d, "
-           "\"truth_errors\": %d, \"seq_ms_per_gate\": %.3f, \"par_ms_per_gate\": %.3f}\n",
-           units, n, par_mismatch, alias_mismatch, truth_errors, 1e3 * (t1 - t0) / total, 1e3 * (t2 - t1) / total);
+           "\"truth_errors\": %d, \"seq_ms_per_gate\": %.3f, \"par_ms_per_gate\": %.3f, \"lanes_before\": %d, "
+           "\"lanes_after_short_threads\": %d, \"short_thread_errors\": %d}\n",
+           units, n, par_mismatch, alias_mismatch, truth_errors, 1e3 * (t1 - t0) / total, 1e3 * (t2 - t1) / total,
+           lanes_before, lanes_after, short_errors);
     delete_gate_bootstrapping_ciphertext_array(total, ali);
     delete_gate_bootstrapping_ciphertext_array(total, par);
     delete_gate_bootstrapping_ciphertext_array(total, seq);
@@ -114,5 +132,5 @@ int main(int argc, char **argv) {
     delete_gate_bootstrapping_ciphertext_array(n, a);
     delete_gate_bootstrapping_secret_keyset(key);
     delete_gate_bootstrapping_parameters(params);
-    return par_mismatch || alias_mismatch || truth_errors ? 1 : 0;
+    return par_mismatch || alias_mismatch || truth_errors || short_errors || lanes_after != lanes_before ? 1 : 0;
 }

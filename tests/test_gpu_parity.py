@@ -153,7 +153,8 @@ def test_chunk_boundaries_bit_exact(ctx, okey, keyset, rng):
 
 
 def test_device_api_rejects_bad_tensors(ctx):
-    """Shapes, dtypes and missing MUX inputs are refused on the host, before any launch."""
+    """Shapes, dtypes, missing MUX inputs and tensors on another GPU are refused on the host,
+    before any launch."""
     torch = _torch()
     B = 4
     a = torch.zeros((B, n), dtype=torch.int32, device="cuda")
@@ -168,6 +169,10 @@ def test_device_api_rejects_bad_tensors(ctx):
     with pytest.raises(T.TfheAmdError):
         ctx.blind_rotate_dev(torch.zeros((B, 2, N), dtype=torch.int32, device="cuda"),
                              torch.zeros((B, 3), dtype=torch.int32, device="cuda"), 4)
+    if torch.cuda.device_count() > 1:   # a tensor on another GPU than the context's
+        other = torch.zeros((B, n), dtype=torch.int32, device="cuda:1")
+        with pytest.raises(T.TfheAmdError):
+            ctx.gate_dev("NAND", a, b, other, b, a, b)
 
 
 def test_empty_batch_is_a_no_op(ctx, keyset, rng):

@@ -1,0 +1,121 @@
+"""Exactness guard of the fp64 FFT blind rotation (include/tfhe_amd.h
+tfhe_amd_guard_stats).  The default kernel rounds each external-product coefficient to the
+nearest integer, which is the exact product only while the FFT error stays below 1/2; every
+launch measures the largest rounding distance per ciphertext and the exact 2-prime NTT kernel
+recomputes the ones at or above 1/4 before their key switch.
+
+CPU: a constructed worst case — a bootstrapping key whose polynomials are all the constant
+2^31 - 1 — drives the fp64 product's rounding distance to 1/2 in the numpy emulation of the
+kernel's data flow (scripts/emu_v6.py) and in the fp64 CPU port, whose unguarded results are
+then wrong on every coefficient, while real keys stay near 0.05.
+GPU: with real keys nothing is recomputed and the distance stays below 1/4; with the threshold
+forced to 0 every ciphertext (gates, MUX halves, circuit rows) is recomputed by the exact kernel
+and the outputs are still the oracle's word for word; with the constructed key the guard fires
+on its own and the outputs equal the oracle's exact ones."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import tfhe_amd as T
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+import emu_v6 as E  # noqa: E402
+
+MAXK = 2**31 - 1
+
+
+def _emu_distance(d, bk):
+    Tb = E.tables()
+    acc = sum(E.fwd(d[p].astype(float), Tb) * (E.fwd(bk[p].astype(float), Tb) / 512) for p in range(4))
+    c = E.inv_dit(acc)
+    exact = np.array([int(x) for x in sum(E.negacyclic(d[p], bk[p]) for p in range(4))], dtype=object)
+    wrong = int(np.sum(np.rint(c).astype(np.int64).astype(object) != exact))
+    return float(np.max(np.abs(c - np.rint(c)))), wrong
+
+
+def test_emulated_worst_case_key_trips_the_guard():
+    r = np.random.default_rng(5)
+    d = r.integers(-512, 512, (4, 1024))
+    real, wrong_real = _emu_distance(d, r.integers(-2**31, 2**31, (4, 1024)))
+    bad, _ = _emu_distance(np.full((4, 1024), -512), np.full((4, 1024), MAXK))
+    assert real < 0.125 and wrong_real == 0
+    assert bad >= 0.25, bad            # the guard's threshold: this step would be recomputed
+
+
+def test_cpu_fft_port_worst_case_key(keyset, rng):
+    """The same fp64 algorithm on the CPU with no guard: the constructed key makes it wrong."""
+    B = 2
+    x_a = rng.integers(-2**31, 2**31, (B, 500), dtype=np.int64).astype(np.int32)
+    x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    bk = np.full_like(keyset.bk, MAXK)
+    f = O.CpuFftKey(bk, keyset.ksk)
+    got = f.woks_batch(1 << 29, x_a, x_b, nthreads=2)
+    want = O.OracleKey(bk, keyset.ksk).woks_batch(1 << 29, x_a, x_b, nthreads=2)
+    assert f.max_round_error() >= 0.25
+    assert not np.array_equal(got[0], want[0])
+
+
+# ---------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+def test_guard_quiet_on_real_keys(ctx, keyset, rng):
+    ctx.guard_stats(reset=True)
+    B = 256
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b)
+    dist, redo = ctx.guard_stats(reset=True)
+    print(f"largest rounding distance over {B} bootstraps: {dist:.4f}")
+    assert redo == 0 and 0.0 < dist < 0.25
+    assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - (x & y))
+
+
+@pytest.mark.gpu
+def test_guard_forced_fallback_bit_exact(ctx, okey, keyset, rng):
+    """Threshold 0: every blind rotation is recomputed by the exact kernel in guard mode —
+    gates, both MUX halves, woKS and circuit rows — and the results are unchanged."""
+    B = 12
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    ctx.guard_stats(reset=True)
+    try:
+        T.set_guard_threshold(0.0)
+        g = ctx.gate_host("XOR", xa, xb, ya, yb)
+        m = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+        u = ctx.woks_host(T.MU, xa, xb)
+        _, redo = ctx.guard_stats(reset=True)
+        C = T.Circuit()
+        i0, i1, i2 = C.inputs(3)
+        outs = [C.gate("MAJ", i0, i1, i2), C.gate("NAND", i0, i1)]
+        got = C.run(ctx, B, {i0: s, i1: x, i2: y}, outs, keyset, rng)
+        _, redo_c = ctx.guard_stats(reset=True)
+    finally:
+        T.set_guard_threshold(0.25)
+    assert redo == B + 2 * B + B and redo_c == 2 * B
+    assert all(np.array_equal(a, b) for a, b in zip(g, okey.gate_batch("XOR", xa, xb, ya, yb)))
+    assert all(np.array_equal(a, b) for a, b in zip(m, okey.gate_batch("MUX", sa, sb, xa, xb, ya, yb)))
+    assert all(np.array_equal(a, b) for a, b in zip(u, okey.woks_batch(T.MU, xa, xb)))
+    assert np.array_equal(got[outs[0]], ((s + x + y) >= 2).astype(int))
+    assert np.array_equal(got[outs[1]], 1 - (s & x))
+
+
+@pytest.mark.gpu
+def test_guard_catches_worst_case_key(keyset, rng):
+    """The constructed key: the fp64 kernel's rounding distance reaches the threshold, the
+    exact kernel recomputes those ciphertexts, and the woKS outputs equal the exact oracle's."""
+    bk = np.full_like(keyset.bk, MAXK)
+    B = 8
+    x_a = rng.integers(-2**31, 2**31, (B, 500), dtype=np.int64).astype(np.int32)
+    x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    c = T.Context(bk, keyset.ksk, device=0)
+    try:
+        u = c.woks_host(T.MU, x_a, x_b)
+        dist, redo = c.guard_stats()
+    finally:
+        c.close()
+    want = O.OracleKey(bk, keyset.ksk).woks_batch(T.MU, x_a, x_b)
+    assert dist >= 0.25 and redo == B, (dist, redo)
+    assert np.array_equal(u[0], want[0]) and np.array_equal(u[1], want[1])
