@@ -29,7 +29,7 @@ namespace tfhe_amd {
 
 namespace {
 
-constexpr int kV2Threads = 128;
+[[maybe_unused]] constexpr int kV2Threads = 128;
 struct V2Shared {
     uint32_t acc[2][kN];               // TLWE accumulator (a, b)
     uint32_t scratch[2][kPadRow];      // one per wave (prime)
@@ -149,6 +149,7 @@ __device__ __forceinline__ void cmux_v2(V2Shared &sh, const V2Args &g, int i, in
 #ifndef TFHE_AMD_V2_MINW
 #define TFHE_AMD_V2_MINW 1     // waves/SIMD floor for the register allocator (A/B builds: 2, 3)
 #endif
+#ifdef TFHE_AMD_EXPERIMENTAL   // v2 / v3 kernels (EXPERIMENTAL=1 builds)
 __global__ __launch_bounds__(kV2Threads, TFHE_AMD_V2_MINW) void k_blind_rotate_v2(V2Args g, int B, BrInput in0, BrInput in1,
                                                                 int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
@@ -376,6 +377,8 @@ __global__ __launch_bounds__(kV3Threads, 3) void k_blind_rotate_v3_debug(V2Args 
 
 // BK (coefficient domain [i][p][c][N]) -> v2 layout [i][s][c][p][v][L][e], j = 16 L + 4 v + e,
 // from the v1 NTT-domain key [i][s][p][c][N] (same values, bit-reversed NTT order j)
+#endif  // TFHE_AMD_EXPERIMENTAL
+
 __global__ __launch_bounds__(256) void k_bk_v1_to_v2(const uint32_t *__restrict__ v1, uint32_t *__restrict__ v2) {
     const int poly = blockIdx.x;   // (i*2 + s)*8 + c*4 + p
     const int p = poly & 3, c = (poly >> 2) & 1, is = poly >> 3;
@@ -444,6 +447,7 @@ hipError_t launch_bk_v1_to_v2(const uint32_t *d_v1, uint32_t *d_v2, hipStream_t 
     return hipGetLastError();
 }
 
+#ifdef TFHE_AMD_EXPERIMENTAL   // v2 / v3 launchers
 hipError_t launch_blind_rotate_v2(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                   int32_t *u_a, int32_t *u_b, hipStream_t s) {
     if (B <= 0) return hipSuccess;
@@ -485,5 +489,7 @@ hipError_t launch_blind_rotate_v2_debug(const DeviceKey &key, int B, int iters, 
     hipLaunchKernelGGL(k_blind_rotate_v2_debug, dim3(B), dim3(kV2Threads), 0, s, v2_args(key), iters, acc, bara);
     return hipGetLastError();
 }
+
+#endif  // TFHE_AMD_EXPERIMENTAL
 
 }  // namespace tfhe_amd

@@ -124,6 +124,7 @@ __device__ __forceinline__ void cmux_step(BrShared &sh, const uint32_t *__restri
     __syncthreads();
 }
 
+#ifdef TFHE_AMD_EXPERIMENTAL   // v1 kernels (EXPERIMENTAL=1 builds)
 __global__ __launch_bounds__(kBrThreads) void k_blind_rotate_v1(
     const uint32_t *__restrict__ bk_ntt, const NttTables *__restrict__ tab, int B,
     BrInput in0, BrInput in1, int32_t mu, int32_t *__restrict__ u_a, int32_t *__restrict__ u_b) {
@@ -189,6 +190,8 @@ __global__ __launch_bounds__(kBrThreads) void k_blind_rotate_debug(
     for (int j = tid; j < 2 * kN; j += kBrThreads) accg[j] = (int32_t)sh.acc[j >> kLogN][j & (kN - 1)];
 }
 
+#endif  // TFHE_AMD_EXPERIMENTAL
+
 // coefficient-domain BK -> NTT domain (Montgomery, 1/N folded): one workgroup per polynomial.
 // Output layout [i][s][p][c][kN]  (analogue of init_LweBootstrappingKeyFFT :60-89).
 __global__ __launch_bounds__(256) void k_bk_to_ntt(const int32_t *__restrict__ bk_coef,
@@ -219,6 +222,7 @@ hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const 
     return hipGetLastError();
 }
 
+#ifdef TFHE_AMD_EXPERIMENTAL   // v1 launchers
 hipError_t launch_blind_rotate(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                int32_t *u_a, int32_t *u_b, hipStream_t s) {
     if (B <= 0) return hipSuccess;
@@ -236,5 +240,7 @@ hipError_t launch_blind_rotate_debug(const DeviceKey &key, int B, int iters, int
                        key.bk_ntt, key.tables, iters, acc, bara);
     return hipGetLastError();
 }
+
+#endif  // TFHE_AMD_EXPERIMENTAL
 
 }  // namespace tfhe_amd

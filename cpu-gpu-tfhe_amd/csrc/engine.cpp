@@ -71,12 +71,23 @@ void build_ntt_tables(NttTables *t) {
 
 static std::atomic<int> g_br_version{-1};
 
+// Product builds carry the default fp64 kernel (v6) and the exact NTT kernel (v4: the guard's
+// fallback and the exact reference generation); EXPERIMENTAL=1 builds add the earlier and
+// experimental generations (v1 LDS radix-2, v2, v3, v5 latency, v7 shared-key) for A/B work.
+static bool br_available(int v) {
+#ifdef TFHE_AMD_EXPERIMENTAL
+    return v >= 0 && v <= 7;
+#else
+    return v == 0 || v == 4 || v == 6;
+#endif
+}
+
 int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
     if (v < 0) {
         const char *e = getenv("TFHE_AMD_BR");
         v = e ? atoi(e) : 0;
-        if (v < 0 || v > 7) v = 0;
+        if (!br_available(v)) v = 0;
         g_br_version.store(v, std::memory_order_relaxed);
     }
     return v;
@@ -99,12 +110,14 @@ static hipError_t run_v6_guarded(const DeviceKey &key, int B, int halves, const 
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
                          int32_t *u_b, hipStream_t s, const Guard *guard) {
     switch (br_version()) {
+#ifdef TFHE_AMD_EXPERIMENTAL
     case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
     case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
     case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
-    case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
     case 7: return launch_blind_rotate_v7(key, B, halves, in, mu, u_a, u_b, s);
+#endif
+    case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     default: return run_v6_guarded(key, B, halves, in, mu, u_a, u_b, s, guard);   // 0, 6
     }
 }
@@ -114,8 +127,10 @@ hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, cons
                                     const Guard *guard) {
     switch (br_version()) {
     case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+#ifdef TFHE_AMD_EXPERIMENTAL
     case 5: return launch_blind_rotate_v5_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     case 7: return launch_blind_rotate_v7_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
+#endif
     default: {
         hipError_t e = launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
         if (e != hipSuccess || !guard || !guard->flags) return e;
@@ -262,6 +277,13 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         HIPCHK(launch_bk_to_fft(d_coef, c->key.bk_fft, c->key.tw6, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(d_coef));
+#ifndef TFHE_AMD_EXPERIMENTAL
+        // product builds: the v1-layout NTT key and the NTT tables only fed the v4 repack
+        HIPCHK(hipFree(c->key.bk_ntt));
+        c->key.bk_ntt = nullptr;
+        HIPCHK(hipFree(c->key.tables));
+        c->key.tables = nullptr;
+#endif
         c->key.has_bk = true;
     }
     if (ksk) {
@@ -318,6 +340,24 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
 }
 
 extern "C" int tfhe_amd_context_device(const TfheAmdContext *c) { return c ? c->device : -1; }
+
+// device bytes held for the key material of a context (the key domains its kernels read)
+extern "C" long long tfhe_amd_context_key_bytes(const TfheAmdContext *c) {
+    if (!c) return TFHE_AMD_E_ARG;
+    const DeviceKey &k = c->key;
+    const long long bk = (long long)kn * kKpl * 2 * kN;   // coefficients per bootstrapping key
+    long long n = 0;
+    if (k.bk_ntt) n += bk * 2 * 4;
+    if (k.bk_v2) n += bk * 2 * 4;
+    if (k.bk_fft) n += bk / 2 * 16;
+    if (k.tw2) n += (long long)kTw2Words * 8;
+    if (k.tw4) n += (long long)kTw4Words * 8;
+    if (k.tw6) n += (long long)kTw6Words * 16;
+    if (k.ksk) n += (long long)kN * kKsT * 3 * kKsRow * 4;
+    if (k.ksk4) n += (long long)ksk_v4_words() * 4;
+    if (k.tables) n += (long long)sizeof(NttTables);
+    return n;
+}
 extern "C" void *tfhe_amd_context_stream(TfheAmdContext *c) { return c ? (void *)c->stream : nullptr; }
 
 extern "C" int tfhe_amd_sync(TfheAmdContext *c) {
@@ -525,12 +565,17 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     HIPCHK(hipSetDevice(c->device));
     ProfScope ps(c, s, true);
     const int v = br_version();
+#ifdef TFHE_AMD_EXPERIMENTAL
     HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
            : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
            : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
            : (v == 4 || v == 5) ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)   // v5 shares v4's math
            : v == 7 ? launch_blind_rotate_v7_debug(c->key, B, iters, acc, bara, s)
                     : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
+#else
+    HIPCHK(v == 4 ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)
+                  : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
+#endif
     return TFHE_AMD_OK;
 }
 
@@ -755,7 +800,7 @@ extern "C" int tfhe_amd_guard_stats(TfheAmdContext *c, double *max_distance, lon
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {
-    if (br_version < 0 || br_version > 7) return TFHE_AMD_E_ARG;
+    if (!br_available(br_version)) return TFHE_AMD_E_ARG;
     g_br_version.store(br_version);
     return TFHE_AMD_OK;
 }

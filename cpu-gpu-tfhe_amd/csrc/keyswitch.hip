@@ -23,6 +23,7 @@ namespace tfhe_amd {
 
 namespace {
 
+#ifdef TFHE_AMD_EXPERIMENTAL   // ks-v1 .. v3 (EXPERIMENTAL=1 builds)
 constexpr int kKsThreads = 512;
 
 __global__ __launch_bounds__(kKsThreads) void k_keyswitch_v1(
@@ -206,6 +207,7 @@ __global__ __launch_bounds__(kKsV2Threads) void k_keyswitch_v3(
         else if (col == kn) res_b[g] = (int32_t)acc[k];
     }
 }
+#endif  // TFHE_AMD_EXPERIMENTAL
 
 // ---------------------------------------------------------------- v4
 // Lane = ciphertext.  A workgroup of 4 waves owns 256 ciphertexts and a 4-column slice of
@@ -532,7 +534,11 @@ int ks_version() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_KS");
         const int x = e ? atoi(e) : 4;
+#ifdef TFHE_AMD_EXPERIMENTAL
         return (x >= 1 && x <= 4) ? x : 4;
+#else
+        return x == 4 ? x : 4;   // ks-v1 .. v3 are in EXPERIMENTAL=1 builds only
+#endif
     }();
     return v;
 }
@@ -541,6 +547,7 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
                             const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,
                             int32_t *res_a, int32_t *res_b, hipStream_t s) {
     if (B <= 0) return hipSuccess;
+#ifdef TFHE_AMD_EXPERIMENTAL
     if (ks_version() == 1) {
         hipLaunchKernelGGL(k_keyswitch_v1, dim3(B), dim3(kKsThreads), 0, s, key.ksk, u_a, u_b, u2_a, u2_b,
                            add_b, res_a, res_b);
@@ -552,7 +559,9 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
         const int blocks = ((B + kKsCt - 1) / kKsCt) * 8;
         hipLaunchKernelGGL(k_keyswitch_v3, dim3(blocks), dim3(kKsV2Threads), 0, s, key.ksk, B, u_a, u_b, u2_a,
                            u2_b, add_b, res_a, res_b);
-    } else if (B <= ks_small_max()) {
+    } else
+#endif
+    if (B <= ks_small_max()) {
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
         hipLaunchKernelGGL(k_keyswitch_small_init<KsPlain>, dim3(B), dim3(512), 0, s, io);
         if (B <= ks_unroll_max())

@@ -76,6 +76,8 @@ def _load():
                                        ctypes.c_int]
     L.tfhe_amd_set_guard_threshold.argtypes = [ctypes.c_double]
     L.tfhe_amd_tier1_lane_count.argtypes = [_VP]
+    L.tfhe_amd_context_key_bytes.restype = ctypes.c_longlong
+    L.tfhe_amd_context_key_bytes.argtypes = [_VP]
     L.tfhe_random_generator_setSeed.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.modSwitchToTorus32.restype = ctypes.c_int32
     L.modSwitchFromTorus32.restype = ctypes.c_int
@@ -105,8 +107,17 @@ def version():
 
 
 def select_kernel(generation):
-    """tfhe_amd_select_kernel: blind-rotation kernel generation 1..7 (A/B and cross-checks; 0 = default)."""
+    """tfhe_amd_select_kernel: blind-rotation kernel generation (0 = default v6, 4 = exact NTT;
+    EXPERIMENTAL=1 builds also 1, 2, 3, 5, 7) for A/B runs and cross-checks."""
     _check(lib.tfhe_amd_select_kernel(int(generation)), "select_kernel")
+
+
+def available_kernels():
+    """The blind-rotation generations this build of the library carries (selection restored)."""
+    cur = version().split("br-v")[1].split(" ")[0]
+    out = [v for v in range(1, 8) if lib.tfhe_amd_select_kernel(v) == 0]
+    lib.tfhe_amd_select_kernel(int(cur) if cur.isdigit() else 0)
+    return out
 
 
 def set_guard_threshold(distance):
@@ -329,6 +340,10 @@ class Context:
     @property
     def stream(self):
         return lib.tfhe_amd_context_stream(self.h)
+
+    def key_bytes(self):
+        """device bytes of this context's key material (tfhe_amd_context_key_bytes)"""
+        return int(lib.tfhe_amd_context_key_bytes(self.h))
 
     def sync(self):
         _check(lib.tfhe_amd_sync(self.h), "sync")

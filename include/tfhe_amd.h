@@ -61,6 +61,9 @@ int tfhe_amd_context_create(const TFheGateBootstrappingCloudKeySet *bk, int devi
 int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk, int device, TfheAmdContext **out);
 int tfhe_amd_context_destroy(TfheAmdContext *ctx);
 int tfhe_amd_context_device(const TfheAmdContext *ctx);
+/* device bytes of the context's key material (the transform-domain bootstrapping keys and the
+ * key-switching key layouts its kernels read) */
+long long tfhe_amd_context_key_bytes(const TfheAmdContext *ctx);
 /* the context's stream as a hipStream_t (void*) */
 void *tfhe_amd_context_stream(TfheAmdContext *ctx);
 int tfhe_amd_sync(TfheAmdContext *ctx);
@@ -137,11 +140,11 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 /* TLWE secret key (int32 [1024]; k = 1), = the extracted LWE key of woKS outputs */
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
-/* Select the blind-rotation kernel generation: 0 = default (v6), 1..5 = exact 2-prime NTT
- * kernels (1 = LDS radix-2 reference kernel, 2 = register-resident NTT with 2 waves per
- * ciphertext, 3 = 4 waves per ciphertext, 4 = v2 layout with a Cooley-Tukey inverse, lazy CRT
- * and a periodic accumulator, 5 = 8 waves per ciphertext), 6 = fp64 FFT external product (the
- * reference's arithmetic; its rounded products equal the exact ones: FFT error < 0.05 << 1/2).
+/* Select the blind-rotation kernel generation: 0 = default (= 6: fp64 FFT external product,
+ * the reference's arithmetic, with the exactness guard above), 4 = the exact 2-prime NTT kernel.
+ * EXPERIMENTAL=1 builds also carry 1 (LDS radix-2 reference kernel), 2 (register-resident NTT,
+ * 2 waves per ciphertext), 3 (4 waves), 5 (8 waves per ciphertext, latency) and 7 (v6 with the
+ * key slice shared through LDS).  Returns TFHE_AMD_E_ARG for a generation this build lacks.
  * env TFHE_AMD_BR=<n> does the same at startup.  For A/B measurements and parity
  * cross-checks; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
