@@ -43,3 +43,13 @@ LweBootstrappingKeyFFT *new_bkfft(const LweBootstrappingKey *bk);
 
 }  // namespace api
 }  // namespace tfhe_amd
+
+// tfhe_api.cpp <-> multi.cpp (multi-device batches)
+// coefficient-domain bootstrapping key of a cloud key (int32 [500][4][2][1024])
+int tfhe_amd_internal_bk_coef(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out);
+// one SoA batch of a gate on the key's Tier-1 device context (this thread's lane)
+int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, int gate, int B, int32_t *res_a,
+                                  int32_t *res_b, const int32_t *a_a, const int32_t *a_b, const int32_t *b_a,
+                                  const int32_t *b_b, const int32_t *c_a, const int32_t *c_b);
+// drops the multi-device context registered for a key (tfhe_gpu_init) when the key is deleted
+void tfhe_amd_internal_forget_multi(const void *bkfft);

@@ -397,6 +397,7 @@ static void delete_bkfft(LweBootstrappingKeyFFT *k) {
     if (!k) return;
     BkFFTImpl *f = bkfft_of(k);
     forget_device_keys(k, f->ks);
+    tfhe_amd_internal_forget_multi(k);
     delete_ksk(f->ks);
     delete f;
 }
@@ -724,6 +725,21 @@ EXPORT void bootsCOPY(LweSample *r, const LweSample *a, const TFheGateBootstrapp
 EXPORT void bootsCONSTANT(LweSample *r, int value, const TFheGateBootstrappingCloudKeySet *bk) {
     const Torus32 MU = modSwitchToTorus32(1, 8);
     lweNoiselessTrivial(r, value ? MU : -MU, bk->params->in_out_params);
+}
+
+int tfhe_amd_internal_bk_coef(const TFheGateBootstrappingCloudKeySet *bk, int32_t *out) {
+    if (!bk || !bk->bkFFT || !out) return TFHE_AMD_E_ARG;
+    const std::vector<int32_t> &c = bkfft_of(bk->bkFFT)->bk_coef;
+    memcpy(out, c.data(), sizeof(int32_t) * c.size());
+    return TFHE_AMD_OK;
+}
+
+int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, int gate, int B, int32_t *res_a,
+                                  int32_t *res_b, const int32_t *a_a, const int32_t *a_b, const int32_t *b_a,
+                                  const int32_t *b_b, const int32_t *c_a, const int32_t *c_b) {
+    if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
+    TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
+    return tfhe_amd_gate_batch_host(l, gate, B, res_a, res_b, a_a, a_b, b_a, b_b, c_a, c_b);
 }
 
 // batched convenience over LweSample arrays (SoA staging on the host)

@@ -78,6 +78,18 @@ def _load():
     L.tfhe_amd_tier1_lane_count.argtypes = [_VP]
     L.tfhe_amd_context_key_bytes.restype = ctypes.c_longlong
     L.tfhe_amd_context_key_bytes.argtypes = [_VP]
+    L.tfhe_amd_multi_create_raw.argtypes = [_I32P, _I32P, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                            ctypes.POINTER(_VP)]
+    L.tfhe_amd_multi_create.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(_VP)]
+    L.tfhe_amd_multi_destroy.argtypes = [_VP]
+    L.tfhe_amd_multi_devices.argtypes = [_VP, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.tfhe_amd_multi_context.restype = _VP
+    L.tfhe_amd_multi_context.argtypes = [_VP, ctypes.c_int]
+    L.tfhe_amd_multi_gate_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_I32P] * 8
+    L.tfhe_amd_shard_range.argtypes = [ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]
+    L.tfhe_gpu_init.argtypes = [_VP, ctypes.c_int]
+    L.tfhe_gpu_boots_batch.argtypes = [ctypes.c_int] + [_I32P] * 8 + [ctypes.c_int, _VP]
     L.tfhe_random_generator_setSeed.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.modSwitchToTorus32.restype = ctypes.c_int32
     L.modSwitchFromTorus32.restype = ctypes.c_int
@@ -434,6 +446,78 @@ class Context:
         _check(lib.tfhe_amd_profile_read(self.h, ctypes.byref(br), ctypes.byref(nb), ctypes.byref(ks),
                                          ctypes.byref(nk)), "profile_read")
         return {"br_ms": br.value, "br_launches": nb.value, "ks_ms": ks.value, "ks_launches": nk.value}
+
+
+# --------------------------------------------------------------------- several GPUs (§8(e))
+
+def shard_range(total, rank, world):
+    """tfhe_amd_shard_range: the library's contiguous shard [lo, hi) (= shard.shard_range)."""
+    lo, hi = ctypes.c_longlong(), ctypes.c_longlong()
+    _check(lib.tfhe_amd_shard_range(int(total), int(rank), int(world), ctypes.byref(lo), ctypes.byref(hi)),
+           "shard_range")
+    return lo.value, hi.value
+
+
+class MultiContext:
+    """TfheAmdMulti: one key replica and worker thread per device; a batch of independent gates
+    is split into contiguous shards, one per device (tfhe_amd_multi_gate_batch_host)."""
+
+    def __init__(self, bk, ksk, devices):
+        self.bk = i32(bk)
+        self.ksk = i32(ksk)
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = _VP()
+        _check(lib.tfhe_amd_multi_create_raw(_p(self.bk), _p(self.ksk), arr, len(self.devices), ctypes.byref(h)),
+               "tfhe_amd_multi_create_raw")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.tfhe_amd_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None):
+        g = GATES[gate] if isinstance(gate, str) else int(gate)
+        ca_a = i32(ca_a); B = ca_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_multi_gate_batch_host(self.h, g, B, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)),
+                                                  _p(i32(cb_a)), _p(i32(cb_b)),
+                                                  _p(None if cc_a is None else i32(cc_a)),
+                                                  _p(None if cc_b is None else i32(cc_b))), "multi_gate_batch_host")
+        return r_a, r_b
+
+    def guard_stats(self, reset=False):
+        """per device slot: (largest rounding distance, ciphertexts recomputed exactly)"""
+        out = []
+        for i in range(len(self.devices)):
+            c = lib.tfhe_amd_multi_context(self.h, i)
+            d = ctypes.c_double(); r = ctypes.c_longlong()
+            _check(lib.tfhe_amd_guard_stats(c, ctypes.byref(d), ctypes.byref(r), int(bool(reset))), "guard_stats")
+            out.append((d.value, r.value))
+        return out
+
+
+def gpu_init(cloud, device_mask):
+    """tfhe_gpu_init(cloud key, device_mask): register a multi-device context for the key."""
+    _check(lib.tfhe_gpu_init(ctypes.c_void_p(cloud), int(device_mask)), "tfhe_gpu_init")
+
+
+def gpu_boots_batch(cloud, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None):
+    """tfhe_gpu_boots_batch over the key's registered devices (SURVEY.md §8(b) Tier-2)."""
+    g = GATES[gate] if isinstance(gate, str) else int(gate)
+    ca_a = i32(ca_a); B = ca_a.shape[0]
+    r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+    _check(lib.tfhe_gpu_boots_batch(g, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)), _p(i32(cb_a)), _p(i32(cb_b)),
+                                    _p(None if cc_a is None else i32(cc_a)), _p(None if cc_b is None else i32(cc_b)),
+                                    B, ctypes.c_void_p(cloud)), "tfhe_gpu_boots_batch")
+    return r_a, r_b
 
 
 # --------------------------------------------------------------------- circuits (§8(f) row 1)

@@ -119,6 +119,39 @@ int tfhe_amd_profile_enable(TfheAmdContext *ctx, int enable);
 int tfhe_amd_profile_read(TfheAmdContext *ctx, double *br_ms, int *br_launches,
                           double *ks_ms, int *ks_launches);
 
+/* ---------------------------------------------------------------- several GPUs
+ * A multi-device context holds one replica of the key per device (uploaded and converted on
+ * each device concurrently) and one worker thread per device.  A batch of independent gates
+ * is split into contiguous shards whose sizes differ by at most one (tfhe_amd_shard_range,
+ * the arithmetic of cpu-gpu-tfhe_amd/shard.py); every device runs its shard through the
+ * single-device host path and writes disjoint rows of the caller's arrays.  No collective.
+ * Generalizes the reference's per-batch chunk loop (gpuParallel/boot-gates.cu:2869-2907) from
+ * one GPU to all of them.  `devices` may repeat a device (several contexts on one GPU). */
+typedef struct TfheAmdMulti TfheAmdMulti;
+int tfhe_amd_multi_create(const TFheGateBootstrappingCloudKeySet *bk, int device_mask, TfheAmdMulti **out);
+int tfhe_amd_multi_create_raw(const int32_t *bk, const int32_t *ksk, const int *devices, int ndev,
+                              TfheAmdMulti **out);
+int tfhe_amd_multi_destroy(TfheAmdMulti *m);
+/* the device list (returns its length; fills up to cap entries) */
+int tfhe_amd_multi_devices(const TfheAmdMulti *m, int *devices, int cap);
+/* the context of device slot i (profiling, guard statistics); owned by the multi-context */
+TfheAmdContext *tfhe_amd_multi_context(TfheAmdMulti *m, int i);
+/* B gates over the devices, host SoA arrays as tfhe_amd_gate_batch_host; synchronous */
+int tfhe_amd_multi_gate_batch_host(TfheAmdMulti *m, int gate, int B, int32_t *res_a, int32_t *res_b,
+                                   const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
+                                   const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b);
+/* shard [lo, hi) of `total` gates for rank of world */
+int tfhe_amd_shard_range(long long total, int rank, int world, long long *lo, long long *hi);
+
+/* SURVEY.md §8(b) Tier-2 names: tfhe_gpu_init builds (or replaces) the multi-device context of
+ * a cloud key over device_mask (bit d = GPU d); tfhe_gpu_boots_batch runs B gates of one kind
+ * (TFHE_GATE_*; c_* for MUX only) over it, or over the key's Tier-1 device when no multi-device
+ * context was registered.  The context is dropped with the key. */
+int tfhe_gpu_init(const TFheGateBootstrappingCloudKeySet *bk, int device_mask);
+int tfhe_gpu_boots_batch(int gate, int32_t *res_a, int32_t *res_b, const int32_t *a_a, const int32_t *a_b,
+                         const int32_t *b_a, const int32_t *b_b, const int32_t *c_a, const int32_t *c_b, int B,
+                         const TFheGateBootstrappingCloudKeySet *bk);
+
 /* Convenience: the same batch over LweSample arrays (Tier-1 structs) with the device
  * context cached per cloud key. */
 int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
