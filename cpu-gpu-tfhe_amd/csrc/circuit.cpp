@@ -513,3 +513,189 @@ extern "C" int tfhe_amd_circuit_dot(TfheAmdCircuit *c, int nterms, int nbits, co
     reduce_columns(c, std::move(col), out);
     return TFHE_AMD_OK;
 }
+
+// ------------------------------------------------------------------ Cipher's remaining operators
+// (cpuParallel/Cipher.cpp: operator> / <= / == :597-644, minimum :314-333, twosComplement
+// :300-311, absolute :483-505, operator/ + divInternal + addSign :507-589), as level-batched
+// circuits: each builder keeps the reference's semantics on its inputs, but replaces the
+// reference's bit-serial gate chains (n dependent gates) by log-depth trees and scans.
+
+namespace {
+
+// Sklansky parallel-prefix carries with an optional carry-in wire (-1: none): returns the
+// carry-out; sum (nullable) gets a + b + cin.  Generate / propagate as in add_prefix; the
+// carry-in is the generate of a virtual bit -1 with propagate 0.
+int prefix_add_cin(TfheAmdCircuit *c, int n, const int *a, const int *b, int cin, int *sum) {
+    std::vector<int> g(n), p(n);
+    for (int i = 0; i < n; ++i) {
+        g[i] = G(c, TFHE_GATE_AND, a[i], b[i]);
+        p[i] = G(c, TFHE_GATE_XOR, a[i], b[i]);
+    }
+    // fold the carry-in into bit 0: g0' = g0 | (p0 & cin).  g0' and p0 are no longer exclusive,
+    // which the combine only needs of the upper block: a block holding bit 0 is always the lower
+    std::vector<int> G_ = g, P_ = p;
+    if (cin >= 0) G_[0] = tfhe_amd_circuit_lincomb(c, kE8, 2, g[0], 1, p[0], 1, cin);
+    for (int d = 1; d < n; d <<= 1) {
+        std::vector<int> Gn = G_, Pn = P_;
+        for (int i = 0; i < n; ++i) {
+            if (!(i & d)) continue;
+            const int j = (i & ~(d - 1)) - 1;
+            Gn[i] = tfhe_amd_circuit_lincomb(c, kE8, 2, G_[i], 1, P_[i], 1, G_[j]);
+            Pn[i] = G(c, TFHE_GATE_AND, P_[i], P_[j]);
+        }
+        G_ = Gn;
+        P_ = Pn;
+    }
+    if (sum) {
+        sum[0] = cin >= 0 ? G(c, TFHE_GATE_XOR, p[0], cin) : p[0];
+        for (int i = 1; i < n; ++i) sum[i] = G(c, TFHE_GATE_XOR, p[i], G_[i - 1]);
+    }
+    return G_[n - 1];
+}
+
+// carry-out of a + ~b (+ 1 if borrow_in_one): a > b (unsigned) without, a >= b with; a tree
+// over the (G, P) pairs, P = XNOR (exclusive with G = a & ~b), log2 n levels
+int carry_compare(TfheAmdCircuit *c, int n, const int *a, const int *b, bool ge) {
+    std::vector<int> Gs(n), Ps(n);
+    for (int i = 0; i < n; ++i) {
+        Gs[i] = G(c, TFHE_GATE_ANDYN, a[i], b[i]);   // a & ~b
+        Ps[i] = G(c, TFHE_GATE_XNOR, a[i], b[i]);    // a ^ ~b
+    }
+    if (ge) Gs[0] = G(c, TFHE_GATE_ORYN, a[0], b[0]);  // with carry-in 1: g0 | p0 = a0 | ~b0
+    while (Gs.size() > 1) {
+        std::vector<int> g2, p2;
+        for (size_t i = 0; i + 1 < Gs.size(); i += 2) {   // (hi = i + 1) o (lo = i)
+            g2.push_back(tfhe_amd_circuit_lincomb(c, kE8, 2, Gs[i + 1], 1, Ps[i + 1], 1, Gs[i]));
+            p2.push_back(Gs.size() > 2 ? G(c, TFHE_GATE_AND, Ps[i + 1], Ps[i]) : -1);
+        }
+        if (Gs.size() & 1) {
+            g2.push_back(Gs.back());
+            p2.push_back(Ps.back());
+        }
+        Gs.swap(g2);
+        Ps.swap(p2);
+    }
+    return Gs[0];
+}
+
+// prefix OR: o[i] = x[0] | ... | x[i - 1] (o[0] = none: -1), Sklansky scan
+std::vector<int> prefix_or_exclusive(TfheAmdCircuit *c, int n, const int *x) {
+    std::vector<int> s(x, x + n);   // inclusive scan
+    for (int d = 1; d < n; d <<= 1) {
+        std::vector<int> t = s;
+        for (int i = 0; i < n; ++i) {
+            if (!(i & d)) continue;
+            const int j = (i & ~(d - 1)) - 1;
+            t[i] = G(c, TFHE_GATE_OR, s[i], s[j]);
+        }
+        s.swap(t);
+    }
+    std::vector<int> o(n, -1);
+    for (int i = 1; i < n; ++i) o[i] = s[i - 1];
+    return o;
+}
+
+// out = cond ? -x : x (two's complement, n bits): out_i = x_i ^ (cond & (x_0 | ... | x_{i-1}))
+// (cond = -1: unconditional negation, twosComplement Cipher.cpp:300-311)
+void cond_negate(TfheAmdCircuit *c, int n, const int *x, int cond, int *out) {
+    const std::vector<int> o = prefix_or_exclusive(c, n, x);
+    out[0] = x[0];
+    for (int i = 1; i < n; ++i) {
+        const int t = cond >= 0 ? G(c, TFHE_GATE_AND, cond, o[i]) : o[i];
+        out[i] = G(c, TFHE_GATE_XOR, x[i], t);
+    }
+}
+
+}  // namespace
+
+// comparison of two n-bit integers (two's complement when is_signed) -> one wire:
+// op 0 a > b, 1 a >= b, 2 a < b, 3 a <= b, 4 a == b, 5 a != b.  operator> (Cipher.cpp:597-609)
+// ripples compareBit_g = MAJ(x, ~y, c) over all bits and fixes the sign with x_msb ^ y_msb;
+// here the carry of a + ~b is a log-depth (G, P) tree and the sign fix one XOR3 row.
+// operator== (:628-644) ORs the bit XORs in a chain; here XNOR then an AND tree.
+extern "C" int tfhe_amd_circuit_compare(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int op,
+                                        int is_signed) {
+    if (!c || nbits <= 0 || !a || !b || op < 0 || op > 5) return TFHE_AMD_E_ARG;
+    if (op >= 4) {
+        std::vector<int> e(nbits);
+        for (int i = 0; i < nbits; ++i) e[i] = G(c, TFHE_GATE_XNOR, a[i], b[i]);
+        while (e.size() > 1) {
+            std::vector<int> e2;
+            for (size_t i = 0; i + 1 < e.size(); i += 2) e2.push_back(G(c, TFHE_GATE_AND, e[i], e[i + 1]));
+            if (e.size() & 1) e2.push_back(e.back());
+            e.swap(e2);
+        }
+        return op == 4 ? e[0] : G(c, TFHE_GATE_NOT, e[0]);
+    }
+    // a > b = carry(a + ~b); a >= b = carry(a + ~b + 1); a < b = b > a; a <= b = b >= a
+    const bool swap = op == 2 || op == 3, ge = op == 1 || op == 3;
+    const int *x = swap ? b : a, *y = swap ? a : b;
+    int r = carry_compare(c, nbits, x, y, ge);
+    if (is_signed) r = G(c, TFHE_GATE_XOR3, r, x[nbits - 1], y[nbits - 1]);
+    return r;
+}
+
+// min / max of two n-bit integers (minimum, Cipher.cpp:314-333: unsigned; is_signed: two's
+// complement): one comparison, then one level of MUXes
+extern "C" int tfhe_amd_circuit_minmax(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int want_max,
+                                       int is_signed, int *out) {
+    if (!c || nbits <= 0 || !a || !b || !out) return TFHE_AMD_E_ARG;
+    const int gt = tfhe_amd_circuit_compare(c, nbits, a, b, 0, is_signed);
+    if (gt < 0) return gt;
+    for (int i = 0; i < nbits; ++i)
+        out[i] = want_max ? G(c, TFHE_GATE_MUX, gt, a[i], b[i]) : G(c, TFHE_GATE_MUX, gt, b[i], a[i]);
+    return TFHE_AMD_OK;
+}
+
+// -x (twosComplement, Cipher.cpp:300-311) and |x| (absolute, :483-505) of an n-bit two's
+// complement integer: a prefix-OR scan, one AND level (abs), one XOR level
+extern "C" int tfhe_amd_circuit_neg(TfheAmdCircuit *c, int nbits, const int *a, int *out) {
+    if (!c || nbits <= 0 || !a || !out) return TFHE_AMD_E_ARG;
+    cond_negate(c, nbits, a, -1, out);
+    return TFHE_AMD_OK;
+}
+extern "C" int tfhe_amd_circuit_abs(TfheAmdCircuit *c, int nbits, const int *a, int *out) {
+    if (!c || nbits <= 0 || !a || !out) return TFHE_AMD_E_ARG;
+    cond_negate(c, nbits, a, a[nbits - 1], out);
+    return TFHE_AMD_OK;
+}
+
+// unsigned restoring division q = a / b, r = a % b (n bits each; b = 0 gives q = all ones,
+// r = a): for i = n - 1 .. 0: R = 2 R + a_i (n + 1 bits), T = R - b, q_i = (R >= b) = the
+// carry-out of R + ~b + 1, R = q_i ? T : R.  The reference's divInternal (Cipher.cpp:526-558)
+// does the same on n-bit signed intermediates; each step here is a parallel-prefix
+// subtraction (depth 2 + log2(n + 1)) plus one MUX level.
+extern "C" int tfhe_amd_circuit_divu(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *q, int *r) {
+    if (!c || nbits <= 0 || !a || !b || !q) return TFHE_AMD_E_ARG;
+    const int n = nbits;
+    const int zero = G(c, TFHE_GATE_CONST, 0), one = G(c, TFHE_GATE_CONST, 1);
+    std::vector<int> R(n, zero), nb(n + 1);
+    for (int i = 0; i < n; ++i) nb[i] = G(c, TFHE_GATE_NOT, b[i]);
+    nb[n] = one;                                   // ~0 of the zero-extended b
+    for (int i = n - 1; i >= 0; --i) {
+        std::vector<int> S(n + 1);                 // 2 R + a_i
+        S[0] = a[i];
+        for (int k = 0; k < n; ++k) S[k + 1] = R[k];
+        std::vector<int> T(n + 1);
+        const int ge = prefix_add_cin(c, n + 1, S.data(), nb.data(), one, T.data());
+        q[i] = ge;
+        for (int k = 0; k < n; ++k) R[k] = G(c, TFHE_GATE_MUX, ge, T[k], S[k]);
+    }
+    if (r)
+        for (int k = 0; k < n; ++k) r[k] = R[k];
+    return TFHE_AMD_OK;
+}
+
+// signed division truncated toward zero (operator/, Cipher.cpp:507-524): |a| / |b| by the
+// restoring divider, then negated when the signs differ (addSign :560-589)
+extern "C" int tfhe_amd_circuit_div(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *q) {
+    if (!c || nbits <= 0 || !a || !b || !q) return TFHE_AMD_E_ARG;
+    std::vector<int> aa(nbits), ab(nbits), uq(nbits);
+    cond_negate(c, nbits, a, a[nbits - 1], aa.data());
+    cond_negate(c, nbits, b, b[nbits - 1], ab.data());
+    const int rc = tfhe_amd_circuit_divu(c, nbits, aa.data(), ab.data(), uq.data(), nullptr);
+    if (rc < 0) return rc;
+    const int sign = G(c, TFHE_GATE_XOR, a[nbits - 1], b[nbits - 1]);
+    cond_negate(c, nbits, uq.data(), sign, q);
+    return TFHE_AMD_OK;
+}

@@ -536,6 +536,13 @@ lib.tfhe_amd_circuit_node.argtypes = [_VP, ctypes.c_int, _IP, _IP, ctypes.POINTE
                                       ctypes.POINTER(ctypes.c_int32), _IP]
 lib.tfhe_amd_circuit_run_dev.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, _VP]
 lib.tfhe_amd_circuit_dot.argtypes = [_VP, ctypes.c_int, ctypes.c_int, _IP, _IP, ctypes.c_int, _IP]
+lib.tfhe_amd_circuit_compare.argtypes = [_VP, ctypes.c_int, _IP, _IP, ctypes.c_int, ctypes.c_int]
+lib.tfhe_amd_circuit_minmax.argtypes = [_VP, ctypes.c_int, _IP, _IP, ctypes.c_int, ctypes.c_int, _IP]
+lib.tfhe_amd_circuit_neg.argtypes = [_VP, ctypes.c_int, _IP, _IP]
+lib.tfhe_amd_circuit_abs.argtypes = [_VP, ctypes.c_int, _IP, _IP]
+lib.tfhe_amd_circuit_divu.argtypes = [_VP, ctypes.c_int, _IP, _IP, _IP, _IP]
+lib.tfhe_amd_circuit_div.argtypes = [_VP, ctypes.c_int, _IP, _IP, _IP]
+CMP = {"GT": 0, "GE": 1, "LT": 2, "LE": 3, "EQ": 4, "NE": 5}
 for _f in ("add", "sub", "add_prefix", "mul"):
     getattr(lib, "tfhe_amd_circuit_" + _f).argtypes = (
         [_VP, ctypes.c_int, _IP, _IP] + ([ctypes.c_int] if _f == "add" else []) + [_IP])
@@ -608,6 +615,37 @@ class Circuit:
         out = (ctypes.c_int * out_bits)()
         self._w(lib.tfhe_amd_circuit_dot(self.h, nt, nb, _ids(fa), _ids(fb), int(out_bits), out), "dot")
         return list(out)
+
+    def compare(self, a, b, op, signed=False):
+        """one wire: a OP b, OP in GT GE LT LE EQ NE (tfhe_amd_circuit_compare)"""
+        return self._w(lib.tfhe_amd_circuit_compare(self.h, len(a), _ids(a), _ids(b), CMP[op], int(signed)),
+                       "compare")
+
+    def minmax(self, a, b, want_max=False, signed=False):
+        out = (ctypes.c_int * len(a))()
+        self._w(lib.tfhe_amd_circuit_minmax(self.h, len(a), _ids(a), _ids(b), int(want_max), int(signed), out),
+                "minmax")
+        return list(out)
+
+    def neg(self, a):
+        out = (ctypes.c_int * len(a))()
+        self._w(lib.tfhe_amd_circuit_neg(self.h, len(a), _ids(a), out), "neg")
+        return list(out)
+
+    def abs(self, a):
+        out = (ctypes.c_int * len(a))()
+        self._w(lib.tfhe_amd_circuit_abs(self.h, len(a), _ids(a), out), "abs")
+        return list(out)
+
+    def divu(self, a, b):
+        q, r = (ctypes.c_int * len(a))(), (ctypes.c_int * len(a))()
+        self._w(lib.tfhe_amd_circuit_divu(self.h, len(a), _ids(a), _ids(b), q, r), "divu")
+        return list(q), list(r)
+
+    def div(self, a, b):
+        q = (ctypes.c_int * len(a))()
+        self._w(lib.tfhe_amd_circuit_div(self.h, len(a), _ids(a), _ids(b), q), "div")
+        return list(q)
 
     def info(self):
         v = [ctypes.c_int() for _ in range(4)]

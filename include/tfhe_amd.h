@@ -240,6 +240,24 @@ int tfhe_amd_circuit_mul(TfheAmdCircuit *c, int nbits, const int *a, const int *
 int tfhe_amd_circuit_dot(TfheAmdCircuit *c, int nterms, int nbits, const int *a, const int *b, int out_bits,
                          int *out);
 
+/* Cipher's remaining operators (cpuParallel/Cipher.cpp) as level-batched circuits:
+ * compare: op 0 a > b, 1 a >= b, 2 a < b, 3 a <= b, 4 a == b, 5 a != b (two's complement when
+ *   is_signed; operator> / <= / ==, :597-644) -> the result wire (log-depth trees);
+ * minmax: min (want_max = 0, minimum :314-333) or max, one comparison + one MUX level;
+ * neg: two's complement (twosComplement :300-311); abs: |a| (absolute :483-505);
+ * divu: unsigned restoring division, q = a / b, r = a % b (r nullable; b = 0: q all ones, r = a);
+ * div: signed division truncated toward zero (operator/, divInternal, addSign :507-589).
+ * All return 0 (or the wire id for compare) or a negative TFHE_AMD_E* code. */
+enum { TFHE_AMD_CMP_GT = 0, TFHE_AMD_CMP_GE = 1, TFHE_AMD_CMP_LT = 2, TFHE_AMD_CMP_LE = 3,
+       TFHE_AMD_CMP_EQ = 4, TFHE_AMD_CMP_NE = 5 };
+int tfhe_amd_circuit_compare(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int op, int is_signed);
+int tfhe_amd_circuit_minmax(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int want_max, int is_signed,
+                            int *out);
+int tfhe_amd_circuit_neg(TfheAmdCircuit *c, int nbits, const int *a, int *out);
+int tfhe_amd_circuit_abs(TfheAmdCircuit *c, int nbits, const int *a, int *out);
+int tfhe_amd_circuit_divu(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *q, int *r);
+int tfhe_amd_circuit_div(TfheAmdCircuit *c, int nbits, const int *a, const int *b, int *q);
+
 #ifdef __cplusplus
 }
 #endif

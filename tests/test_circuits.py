@@ -181,3 +181,142 @@ def test_noise_margins_gpu(ctx, keyset, rng):
     print(f"bootstrapped output noise sigma = 2^{np.log2(sigma):.2f}; margins (sigmas): "
           + ", ".join(f"{k} {v:.1f}" for k, v in margins.items()))
     assert min(margins.values()) > 6.0
+
+
+# ---------------------------------------------------------------- Cipher's remaining operators
+
+def _signed(v, n):
+    v = np.asarray(v, dtype=np.int64) & (2**n - 1)
+    return np.where(v >= 2**(n - 1), v - 2**n, v)
+
+
+CMP_F = {"GT": np.greater, "GE": np.greater_equal, "LT": np.less, "LE": np.less_equal,
+         "EQ": np.equal, "NE": np.not_equal}
+
+
+def _cmp_inputs(rng, n, k=300):
+    x = rng.integers(0, 2**n, k)
+    y = rng.integers(0, 2**n, k)
+    e, l1, m1 = k // 5, 3 * k // 10, 2 * k // 5
+    y[:e] = x[:e]                                     # equal pairs
+    y[e:l1] = x[e:l1] ^ 1                             # differ in the lsb only
+    y[l1:m1] = x[l1:m1] ^ (1 << (n - 1))              # differ in the msb only
+    x[m1:m1 + 2] = [0, 2**n - 1]
+    y[m1:m1 + 2] = [2**n - 1, 0]
+    return x, y
+
+
+@pytest.mark.parametrize("n", [1, 3, 8, 16])
+@pytest.mark.parametrize("signed", [False, True])
+def test_compare_plain(n, signed, rng):
+    """operator> / <= / == (Cipher.cpp:597-644) and the other three, unsigned and two's
+    complement, as log-depth circuits."""
+    if signed and n == 1:
+        pytest.skip("a 1-bit two's complement integer is only a sign")
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    outs = {op: C.compare(a, b, op, signed) for op in CMP_F}
+    x, y = _cmp_inputs(rng, n)
+    val = C.eval_plain({**_bits(a, x, n), **_bits(b, y, n)})
+    xv, yv = (_signed(x, n), _signed(y, n)) if signed else (x, y)
+    for op, w in outs.items():
+        assert np.array_equal(val[w], CMP_F[op](xv, yv).astype(int)), op
+    if n == 16:
+        assert C.info()["depth"] <= 2 + int(np.ceil(np.log2(n))) + 1
+
+
+@pytest.mark.parametrize("n", [4, 16])
+@pytest.mark.parametrize("signed", [False, True])
+def test_minmax_plain(n, signed, rng):
+    """minimum (Cipher.cpp:314-333, unsigned) and max, also two's complement."""
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    lo, hi = C.minmax(a, b, False, signed), C.minmax(a, b, True, signed)
+    x, y = _cmp_inputs(rng, n)
+    val = C.eval_plain({**_bits(a, x, n), **_bits(b, y, n)})
+    xv, yv = (_signed(x, n), _signed(y, n)) if signed else (x, y)
+    got_lo, got_hi = _value(val, lo), _value(val, hi)
+    if signed:
+        got_lo, got_hi = _signed(got_lo, n), _signed(got_hi, n)
+    assert np.array_equal(got_lo, np.minimum(xv, yv)) and np.array_equal(got_hi, np.maximum(xv, yv))
+
+
+@pytest.mark.parametrize("n", [2, 8, 16])
+def test_neg_abs_plain(n, rng):
+    """twosComplement (Cipher.cpp:300-311) and absolute (:483-505), two's complement mod 2^n."""
+    C = T.Circuit()
+    a = C.inputs(n)
+    ng, ab = C.neg(a), C.abs(a)
+    x = rng.integers(0, 2**n, 300)
+    x[:4] = [0, 1, 2**(n - 1), 2**n - 1]
+    val = C.eval_plain(_bits(a, x, n))
+    xs = _signed(x, n)
+    assert np.array_equal(_value(val, ng), (-xs) % 2**n)
+    assert np.array_equal(_value(val, ab), np.abs(xs) % 2**n)
+
+
+@pytest.mark.parametrize("n", [1, 4, 8])
+def test_divu_plain(n, rng):
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    q, r = C.divu(a, b)
+    x = rng.integers(0, 2**n, 300)
+    y = rng.integers(1, 2**n, 300)
+    x[:3] = [2**n - 1, 0, 2**n - 1]
+    y[:3] = [1, 1, 2**n - 1]
+    val = C.eval_plain({**_bits(a, x, n), **_bits(b, y, n)})
+    assert np.array_equal(_value(val, q), x // y) and np.array_equal(_value(val, r), x % y)
+
+
+@pytest.mark.parametrize("n", [4, 8, 16])
+def test_signed_div_plain(n, rng):
+    """operator/ (Cipher.cpp:507-589): |a| / |b| by restoring division, negated when the signs
+    differ: truncation toward zero, mod 2^n."""
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    q = C.div(a, b)
+    x = rng.integers(0, 2**n, 200)
+    y = rng.integers(0, 2**n, 200)
+    y[y == 0] = 1
+    x[:4] = [2**(n - 1), 2**(n - 1), 2**n - 1, 5 % 2**n]       # -2^(n-1) / -1 wraps
+    y[:4] = [2**n - 1, 1, 2**n - 1, 2**n - 3 if n > 2 else 1]
+    val = C.eval_plain({**_bits(a, x, n), **_bits(b, y, n)})
+    xs, ys = _signed(x, n), _signed(y, n)
+    want = np.array([(-1 if (p < 0) != (d < 0) else 1) * (abs(int(p)) // abs(int(d))) for p, d in zip(xs, ys)])
+    assert np.array_equal(_value(val, q), want % 2**n)
+
+
+@pytest.mark.gpu
+def test_cipher_operators_gpu(ctx, keyset, rng):
+    """The new builders on the MI355X, 16-bit operands, 48 instances per launch: signed >,
+    unsigned ==, minimum, absolute and signed division decrypt to the integer results."""
+    n, B = 16, 48
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    gt = C.compare(a, b, "GT", True)
+    eq = C.compare(a, b, "EQ")
+    mn = C.minmax(a, b)
+    ab = C.abs(a)
+    x, y = _cmp_inputs(rng, n, B)
+    outs = [gt, eq] + mn + ab
+    got = C.run(ctx, B, {**_bits(a, x, n), **_bits(b, y, n)}, outs, keyset, rng)
+    xs, ys = _signed(x, n), _signed(y, n)
+    assert np.array_equal(got[gt], (xs > ys).astype(int))
+    assert np.array_equal(got[eq], (x == y).astype(int))
+    assert np.array_equal(_value(got, mn), np.minimum(x, y))
+    assert np.array_equal(_value(got, ab), np.abs(xs) % 2**n)
+
+
+@pytest.mark.gpu
+def test_signed_division_gpu(ctx, keyset, rng):
+    n, B = 8, 32
+    C = T.Circuit()
+    a, b = C.inputs(n), C.inputs(n)
+    q = C.div(a, b)
+    x = rng.integers(0, 2**n, B)
+    y = rng.integers(1, 2**n, B)
+    got = C.run(ctx, B, {**_bits(a, x, n), **_bits(b, y, n)}, q, keyset, rng)
+    xs, ys = _signed(x, n), _signed(y, n)
+    want = np.array([(-1 if (p < 0) != (d < 0) else 1) * (abs(int(p)) // abs(int(d))) for p, d in zip(xs, ys)])
+    assert np.array_equal(_value(got, q), want % 2**n)
+    print(f"8-bit signed division circuit: depth {C.info()['depth']}, {C.info()['bootstraps']} bootstraps")
