@@ -2,6 +2,7 @@
 
   config 3: 32-bit ripple-carry encrypted addition (Cipher.cpp operator+ path)
   config 4: 16-bit x 16-bit encrypted multiplication, batch 256 (multiplyLweSamples path)
+  plus Cipher's other operators as circuits: signed >, ==, minimum, signed division (16-bit)
 
 Each circuit is built once (csrc/circuit.cpp), inputs are encrypted under the seeded keys and
 resident in HBM, and the timed region is the whole circuit evaluation (every level's blind
@@ -69,6 +70,15 @@ def main():
     rng = np.random.default_rng(7)
     add = (lambda x, y: x + y)
 
+    def sgn(v):
+        v = np.asarray(v, dtype=np.int64)
+        return np.where(v >= 2**15, v - 2**16, v)
+
+    def sdiv(x, y):   # truncation toward zero, mod 2^16 (y = 0 gives what the circuit gives: skipped)
+        xs, ys = sgn(x), sgn(y)
+        q = [(-1 if (p < 0) != (d < 0) else 1) * (abs(int(p)) // abs(int(d))) if d else -1 for p, d in zip(xs, ys)]
+        return np.array(q, dtype=np.int64) % 2**16
+
     def ripple(C, a, b):
         s, co = C.add(a, b)
         return s + [co]
@@ -84,6 +94,14 @@ def main():
         ("config4: 16x16 multiply, batch 256", lambda C, a, b: C.mul(a, b), 16, 256 if not args.quick else 16,
          lambda x, y: x * y),
         ("16x16 multiply, batch 1", lambda C, a, b: C.mul(a, b), 16, 1, lambda x, y: x * y),
+        ("16-bit signed a > b (operator>)", lambda C, a, b: [C.compare(a, b, "GT", True)], 16, 1,
+         lambda x, y: (sgn(x) > sgn(y)).astype(np.int64)),
+        ("16-bit a == b (operator==)", lambda C, a, b: [C.compare(a, b, "EQ")], 16, 1,
+         lambda x, y: (x == y).astype(np.int64)),
+        ("16-bit minimum", lambda C, a, b: C.minmax(a, b), 16, 1, np.minimum),
+        ("16-bit signed division (operator/)", lambda C, a, b: C.div(a, b), 16, 1, sdiv),
+        ("16-bit signed division, batch 256", lambda C, a, b: C.div(a, b), 16, 256 if not args.quick else 16,
+         sdiv),
     ]
     for name, build, nbits, B, ref in cases:
         r = run_case(T, torch, ctx, K, name, build, nbits, B, args.reps, rng, ref)

@@ -167,3 +167,49 @@ def test_two_rank_gloo_scatter_evaluate_gather():
         assert p.exitcode == 0
     assert res[0][1] == [3] and res[1][1] == [2]          # contiguous shards of 5 over 2 ranks
     assert res[0][2] is True and res[0][3] is True
+
+
+def _matmat_worker(rank, world, port, out):
+    """each rank evaluates its block of output rows of C = A B (plaintext, the engine's own
+    torus arithmetic); blocks are gathered here only to check the whole product."""
+    import numpy as np
+    import torch.distributed as dist
+    import matmat
+    import tfhe_amd as T
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(13)
+    m, k, n, nbits = 5, 3, 4, 4
+    A = rng.integers(0, 2**nbits, (m, k))
+    Bm = rng.integers(0, 2**nbits, (k, n))
+    lo, hi = matmat.shard_rows(m, rank, world)
+    C, a_w, b_w, c_w = matmat.build(T, k, nbits)
+    val = C.eval_plain(matmat.instance_inputs(T, a_w, b_w, A[lo:hi], Bm, nbits))
+    blk = np.asarray(T.int_of([val[w] for w in c_w])).reshape(hi - lo, n)
+    got = [None] * world
+    dist.all_gather_object(got, (lo, hi, blk.tolist()))
+    out.put((rank, got, ((A @ Bm) % 2**nbits).tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_matmat_row_blocks():
+    """C = A B mod 2^nbits (the reference's single-precision BOOTS_matrixMultiplication) with
+    row blocks of C on two gloo ranks: the blocks assemble to the integer product."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_matmat_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got, want in res:
+        full = []
+        for lo, hi, blk in sorted(got):
+            assert len(blk) == hi - lo
+            full += blk
+        assert full == want
