@@ -6,6 +6,7 @@
 
 #include "params.h"
 #include "../../include/tfhe/tfhe.h"
+#include "../../include/tfhe_amd.h"
 
 namespace tfhe_amd {
 namespace api {
@@ -51,5 +52,7 @@ int tfhe_amd_internal_bk_coef(const TFheGateBootstrappingCloudKeySet *bk, int32_
 int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, int gate, int B, int32_t *res_a,
                                   int32_t *res_b, const int32_t *a_a, const int32_t *a_b, const int32_t *b_a,
                                   const int32_t *b_b, const int32_t *c_a, const int32_t *c_b);
+// the extracted samples of a context's last gate batch (<= one round), halves x B rows of 1024
+int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a);
 // drops the multi-device context registered for a key (tfhe_gpu_init) when the key is deleted
 void tfhe_amd_internal_forget_multi(const void *bkfft);

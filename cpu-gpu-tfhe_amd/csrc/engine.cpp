@@ -741,6 +741,17 @@ extern "C" int tfhe_amd_keyswitch_batch_host(TfheAmdContext *c, int B, const int
     return single_input_host(c, OP_KS, B, 0, u_a, u_b, res_a, res_b);
 }
 
+// The extracted samples (key-switch inputs) of this context's last gate batch of at most one
+// round (unsliced host path), halves x B rows of kN words: the Tier-1 API derives the
+// key-switched output's current_variance from their digits (tfhe_api.cpp ks_variance).
+int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a) {
+    if (!c || B <= 0 || halves < 1 || halves > 2 || B > c->cap) return TFHE_AMD_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(u_a, c->u_a, sizeof(int32_t) * (size_t)halves * B * kN, hipMemcpyDeviceToHost));
+    return TFHE_AMD_OK;
+}
+
 // a second context on the same GPU sharing `primary`'s key (own stream + scratch):
 // used for per-thread lanes of the Tier-1 API
 TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {

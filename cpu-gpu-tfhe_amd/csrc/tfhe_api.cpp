@@ -670,23 +670,54 @@ static void check(int rc, const char *what) {
     }
 }
 
+// current_variance of a key-switched sample, as the reference computes it: lweKeySwitch
+// (lwe-keyswitch-functions.cu:955-987) starts from lweNoiselessTrivial (variance 0) and every
+// lweSubTo of a key-switching-key row (lweKeySwitchTranslate_fromArray :101-127) adds that row's
+// variance (lwe-functions.cu:150), in the same i, j order (so the double sum is the same).
+// Bookkeeping only: excluded from the Torus32 parity.
+static double ks_variance(const LweKeySwitchKey *ks, const int32_t *u_a) {
+    const uint32_t prec = 1u << (32 - (1 + ks->basebit * ks->t));
+    const uint32_t mask = (uint32_t)ks->base - 1;
+    double v = 0.;
+    for (int i = 0; i < ks->n; ++i) {
+        const uint32_t aibar = (uint32_t)u_a[i] + prec;
+        for (int j = 0; j < ks->t; ++j) {
+            const uint32_t aij = (aibar >> (32 - (j + 1) * ks->basebit)) & mask;
+            if (aij) v += ks->ks[i][j][aij].current_variance;
+        }
+    }
+    return v;
+}
+
+// the key-switch input of a lane's last gate batch (one sample, halves = 2 for MUX: u1 + u2)
+static void ks_input_of_last(TfheAmdContext *l, int B, int halves, std::vector<int32_t> &u) {
+    u.resize((size_t)halves * B * kN);
+    check(tfhe_amd_internal_last_extracted(l, B, halves, u.data()), "variance bookkeeping");
+    if (halves == 2)
+        for (size_t j = 0; j < (size_t)B * kN; ++j)
+            u[j] = (int32_t)((uint32_t)u[j] + (uint32_t)u[(size_t)B * kN + j]);
+}
+
 EXPORT void tfhe_bootstrap_woKS_FFT(LweSample *result, const LweBootstrappingKeyFFT *bk, Torus32 mu,
                                     const LweSample *x) {
     TfheAmdContext *l = lane_for(bk, nullptr);
     check(tfhe_amd_bootstrap_woks_batch_host(l, 1, mu, x->a, &x->b, result->a, &result->b), "tfhe_bootstrap_woKS_FFT");
-    result->current_variance = 0.;   // bookkeeping only (excluded from parity)
+    // the reference's extraction (lwe.cu:41-56, 227-237) leaves current_variance as it was
 }
 
 EXPORT void tfhe_bootstrap_FFT(LweSample *result, const LweBootstrappingKeyFFT *bk, Torus32 mu, const LweSample *x) {
     TfheAmdContext *l = lane_for(bk, nullptr);
     check(tfhe_amd_bootstrap_batch_host(l, 1, mu, x->a, &x->b, result->a, &result->b), "tfhe_bootstrap_FFT");
-    result->current_variance = 0.;
+    std::vector<int32_t> u;
+    ks_input_of_last(l, 1, 1, u);
+    result->current_variance = ks_variance(bk->ks, u.data());
 }
 
 EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const LweSample *sample) {
     TfheAmdContext *l = lane_for(nullptr, ks);
+    const double v = ks_variance(ks, sample->a);   // before: result may alias sample
     check(tfhe_amd_keyswitch_batch_host(l, 1, sample->a, &sample->b, result->a, &result->b), "lweKeySwitch");
-    result->current_variance = 0.;
+    result->current_variance = v;
 }
 
 // ------------------------------------------------------------------ gates
@@ -697,7 +728,9 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     check(tfhe_amd_gate_batch_host(l, gate, 1, r->a, &r->b, a->a, &a->b, b->a, &b->b, c ? c->a : nullptr,
                                    c ? &c->b : nullptr),
           "gate");
-    r->current_variance = 0.;
+    std::vector<int32_t> u;   // every gate ends in lweKeySwitch (boot-gates.cu:98-448)
+    ks_input_of_last(l, 1, gate == TFHE_GATE_MUX ? 2 : 1, u);
+    r->current_variance = ks_variance(bk->bkFFT->ks, u.data());
 }
 
 EXPORT void bootsNAND(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_NAND, r, a, b, nullptr, bk); }
@@ -758,12 +791,22 @@ EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a,
         memcpy(ba + (size_t)i * kn, b[i].a, kn * 4); bb[i] = b[i].b;
         if (c) { memcpy(ca + (size_t)i * kn, c[i].a, kn * 4); cb[i] = c[i].b; }
     }
-    int rc = tfhe_amd_gate_batch_host(l, gate, B, ra, rb, aa, ab, ba, bb, c ? ca : nullptr, c ? cb : nullptr);
-    if (rc) return rc;
+    // in rounds of at most 1024 gates (the unsliced host path), so that each round's key-switch
+    // inputs are still in the lane's scratch for the variance bookkeeping
+    const int halves = gate == TFHE_GATE_MUX ? 2 : 1;
+    std::vector<int32_t> u;
+    for (int s0 = 0; s0 < B; s0 += 1024) {
+        const int n = B - s0 < 1024 ? B - s0 : 1024;
+        const size_t o = (size_t)s0 * kn;
+        int rc = tfhe_amd_gate_batch_host(l, gate, n, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
+                                          c ? ca + o : nullptr, c ? cb + s0 : nullptr);
+        if (rc) return rc;
+        ks_input_of_last(l, n, halves, u);
+        for (int i = 0; i < n; i++) result[s0 + i].current_variance = ks_variance(bk->bkFFT->ks, u.data() + (size_t)i * kN);
+    }
     for (int i = 0; i < B; i++) {
         memcpy(result[i].a, ra + (size_t)i * kn, kn * 4);
         result[i].b = rb[i];
-        result[i].current_variance = 0.;
     }
     return TFHE_AMD_OK;
 }

@@ -1,7 +1,8 @@
 // ref_driver.cpp — TEST INFRASTRUCTURE ONLY (our own code, not reference code).
 // Flat-array C entry points that call the reference's OWN compiled leaf sources
 // (gpuParallel/{numeric-functions,multiplication,lwe-functions,lwesamples,lwekey,
-// lweparams}.cu, built in place by oracle/build_ref.sh into oracle/_ref/libtfheref.so).
+// lweparams,tgsw,tlwe,lwekeyswitch}.cu, built in place by oracle/build_ref.sh into
+// oracle/_ref/libtfheref.so).
 // Used only to generate the golden fixtures under tests/golden/ and, when the
 // reference is present, to re-check the oracle directly.
 #include <cstring>
@@ -14,6 +15,10 @@
 #include "lwekey.h"
 #include "lwesamples.h"
 #include "lwe-functions.h"
+#include "tlwe.h"
+#include "tgsw.h"
+#include "lwekeyswitch.h"
+#include <vector>
 EXPORT void tfhe_random_generator_setSeed(uint32_t* values, int size);  // numeric-functions.cu:16
 
 extern "C" {
@@ -84,6 +89,30 @@ void ref_lwe_op(int op, int n, int32_t* r_a, int32_t* r_b, const int32_t* s_a, i
     case 5: lweNegate(&r, &s, &params); break;
     }
     std::memcpy(r_a, r.a, n * 4); *r_b = r.b;
+}
+
+// tgsw.cu:7-29 TGswParams over tlwe.cu's TLweParams(N, k): the gadget h[] (l entries), the
+// decomposition offset, kpl, Bg, halfBg, maskMod
+void ref_tgsw_params(int l, int Bgbit, int N, int k, int32_t* h_out, uint32_t* offset_out, int32_t* ints_out) {
+    TLweParams tp(N, k, 0.0, 1.0);
+    TGswParams gp(l, Bgbit, &tp);
+    for (int i = 0; i < l; i++) h_out[i] = gp.h[i];
+    *offset_out = gp.offset;
+    ints_out[0] = gp.kpl; ints_out[1] = gp.Bg; ints_out[2] = gp.halfBg; ints_out[3] = gp.maskMod;
+}
+
+// lwekeyswitch.cu:3-18: the row of ks0_raw that ks[i][j][h] addresses, for i < n, j < t,
+// h < 2^basebit (pointer arithmetic on an unconstructed raw block: the constructor only
+// builds the index arrays)
+void ref_ksk_index(int n, int t, int basebit, int32_t* out) {
+    const int base = 1 << basebit;
+    std::vector<char> raw(sizeof(LweSample) * (size_t)n * t * base);
+    LweSample* ks0 = reinterpret_cast<LweSample*>(raw.data());
+    LweParams op(500, 0.0, 1.0);
+    LweKeySwitchKey key(n, t, basebit, &op, ks0);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < t; j++)
+            for (int h = 0; h < base; h++) out[((size_t)i * t + j) * base + h] = (int32_t)(key.ks[i][j] + h - ks0);
 }
 
 }

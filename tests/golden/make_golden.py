@@ -1,6 +1,7 @@
 """Generate the golden fixtures in tests/golden/ from the reference's OWN compiled leaf
 sources (oracle/_ref/libtfheref.so, built by oracle/build_ref.sh from
-/root/reference/gpuParallel/{numeric-functions,multiplication,lwe-functions,...}.cu).
+/root/reference/gpuParallel/{numeric-functions,multiplication,lwe-functions,...,tgsw,tlwe,
+lwekeyswitch}.cu).
 
 Run in the build container (the reference is not on the GPU box):
     oracle/build_ref.sh && python tests/golden/make_golden.py
@@ -112,7 +113,20 @@ def main():
     out["lweop_out_a"] = oa
     out["lweop_out_b"] = ob
 
-    # (5) struct layouts of the reference's own headers (oracle/ref_layout.cpp)
+    # (5) gadget decomposition constants (tgsw.cu:7-29 over tlwe.cu's TLweParams) and the
+    # key-switching key index map (lwekeyswitch.cu:3-18) at the default parameters
+    h = np.zeros(2, np.int32)
+    off = ctypes.c_uint32(0)
+    ints = np.zeros(4, np.int32)
+    ref.ref_tgsw_params(2, 10, N, 1, p(h), ctypes.byref(off), p(ints))
+    out["tgsw_h"] = h
+    out["tgsw_offset"] = np.array([off.value], np.uint32)
+    out["tgsw_kpl_bg_halfbg_maskmod"] = ints
+    idx = np.zeros(N * 8 * 4, np.int32)
+    ref.ref_ksk_index(N, 8, 2, p(idx))
+    out["ksk_index"] = idx
+
+    # (6) struct layouts of the reference's own headers (oracle/ref_layout.cpp)
     import json
     import subprocess
     lay = subprocess.check_output([os.path.join(REPO, "oracle", "_ref", "ref_layout")]).decode()

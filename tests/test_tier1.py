@@ -35,3 +35,60 @@ def test_tier1_threads_and_aliasing_gpu():
     assert out["par_mismatch"] == 0 and out["alias_mismatch"] == 0 and out["truth_errors"] == 0, out
     # threads that exit give their lanes back (no stream / scratch / pinned-memory leak per thread)
     assert out["short_thread_errors"] == 0 and out["lanes_after_short_threads"] == out["lanes_before"], out
+
+
+@pytest.mark.gpu
+def test_tier1_current_variance_as_reference(keyset, okey, rng):
+    """current_variance after bootsNAND / bootsMUX (Tier-1, through the C ABI): the reference's
+    lweKeySwitch restarts it at 0 and adds the variance of every key-switching-key row its
+    non-zero digits select (lwe-keyswitch-functions.cu:101-127, 955-987; lwe-functions.cu:150),
+    in i, j order — recomputed here from the oracle's exact key-switch input and the row
+    variances of the key's own structs."""
+    import ctypes
+    import numpy as np
+    import tfhe_amd as T
+
+    class LweSample(ctypes.Structure):
+        _fields_ = [("a", ctypes.POINTER(ctypes.c_int32)), ("b", ctypes.c_int32), ("current_variance", ctypes.c_double)]
+    P = ctypes.c_void_p
+    lib = T.lib
+    lib.bootsNAND.argtypes = [P, P, P, P]
+    lib.bootsMUX.argtypes = [P, P, P, P, P]
+    cloud = keyset.cloud
+    bkfft = P.from_address(cloud + 16).value                 # cloud->bkFFT
+    ks = P.from_address(bkfft + 40).value                    # bkFFT->ks
+    ks0 = P.from_address(ks + 24).value                      # ks->ks0_raw
+    rows = (LweSample * (1024 * 8 * 4)).from_address(ks0)
+    row_var = np.array([rows[r].current_variance for r in range(1024 * 8 * 4)])
+
+    def expected(u_a):
+        v = 0.0
+        for i in range(1024):
+            aibar = (int(u_a[i]) + (1 << 15)) & 0xFFFFFFFF
+            for j in range(8):
+                aij = (aibar >> (30 - 2 * j)) & 3
+                if aij:
+                    v += row_var[(i * 8 + j) * 4 + aij]
+        return v
+
+    arr = lib.new_gate_bootstrapping_ciphertext_array(4, P(keyset.params))
+    s = (LweSample * 4).from_address(arr)
+    bits = rng.integers(0, 2, 3)
+    enc = [keyset.encrypt(np.array([x]), rng) for x in bits]
+    for k, (a, b) in enumerate(enc):
+        ctypes.memmove(s[k].a, a[0].ctypes.data, 4 * 500)
+        s[k].b = int(b[0])
+    addr = [ctypes.addressof(s[k]) for k in range(4)]
+    lib.bootsNAND(P(addr[3]), P(addr[0]), P(addr[1]), P(cloud))
+    t_a = (-(enc[0][0][0].astype(np.int64)) - enc[1][0][0]).astype(np.int64)
+    t_b = np.int64(1 << 29) - enc[0][1][0] - enc[1][1][0]
+    u_a, _ = okey.woks_batch(1 << 29, t_a[None, :], np.array([t_b]))
+    assert s[3].current_variance == expected(u_a[0]) and s[3].current_variance > 0
+    lib.bootsMUX(P(addr[3]), P(addr[0]), P(addr[1]), P(addr[2]), P(cloud))
+    u1, _ = okey.woks_batch(1 << 29, (enc[0][0][0].astype(np.int64) + enc[1][0][0])[None, :],
+                            np.array([np.int64(-(1 << 29)) + enc[0][1][0] + enc[1][1][0]]))
+    u2, _ = okey.woks_batch(1 << 29, (-enc[0][0][0].astype(np.int64) + enc[2][0][0])[None, :],
+                            np.array([np.int64(-(1 << 29)) - enc[0][1][0] + enc[2][1][0]]))
+    usum = (u1[0].astype(np.int64) + u2[0]).astype(np.int64)
+    assert s[3].current_variance == expected(usum)
+    lib.delete_gate_bootstrapping_ciphertext_array(4, arr)
