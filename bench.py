@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
-    ap.add_argument("--extra-batches", default="1,4096", help="per-GPU batch sizes also timed ('' = none)")
+    ap.add_argument("--extra-batches", default="1,4096", help="per-GPU batch sizes also timed ('none' = none)")
     ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
@@ -344,7 +344,7 @@ def main():
 
     # the metric's other batch sizes (per GPU, weak scaling like the headline)
     extras = {}
-    for s in (v for v in args.extra_batches.split(",") if v.strip()):
+    for s in (v for v in args.extra_batches.split(",") if v.strip() and v.strip() not in ("none", "''")):
         b = int(s)
         if b == B or b <= 0:
             continue

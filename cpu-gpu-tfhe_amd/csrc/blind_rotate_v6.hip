@@ -131,18 +131,27 @@ __device__ __forceinline__ void set_prio_level(unsigned lvl) {
 }
 
 
+#ifdef TFHE_AMD_DIAG_NOTW
+__device__ __forceinline__ Tw4 diag_tw(int L) {
+    const double x = 0.70710678118654752 + 1e-9 * L;
+    return Tw4{Cx{x, -x}, Cx{-x, x}, Cx{x, x}, Cx{-x, -x}};
+}
+#endif
+
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
 template <int WAVES>
 __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int L,
-                                        uint32_t (&acc)[16], double &mx V6_STAMPS_PARAM) {
+                                        uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
     double2 *X = sh.X[w];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
     const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
+#ifndef TFHE_AMD_DIAG_NOEXT   // timing diagnostic (wrong results): no accumulator-extension stores
     write_ext(E, acc, L);
+#endif
     wave_sync();
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
@@ -167,12 +176,17 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     }
     wave_sync();
     V6_STAMP(0);
-    fft_fwd_AB_t<2>(D, X, tA, tw7_fwdB(sh.tw, L), L);
+#ifdef TFHE_AMD_DIAG_NOTW   // timing diagnostic (wrong results): twiddles from registers, no LDS loads
+#define TW7(fn) diag_tw(L)
+#else
+#define TW7(fn) fn(sh.tw, L)
+#endif
+    fft_fwd_AB_t<2>(D, X, tA, TW7(tw7_fwdB), L);
     V6_STAMP(1);
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC, the hand-over and the barrier.
-    const Tw4 tC = tw7_fwdC(sh.tw, L);
+    const Tw4 tC = TW7(tw7_fwdC);
     Cx Y[8];
     // (issuing them at the top of the step instead, in flight for the whole forward transform,
     // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
@@ -183,7 +197,9 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     V6_STAMP(2);
     load_bk(bv, bk, w);
     __builtin_amdgcn_sched_barrier(0);
+#ifndef TFHE_AMD_DIAG_NOHAND   // timing diagnostic (wrong results): no partial-sum hand-off
     store_C(X, Y, L);
+#endif
     // the second MAC runs after the barrier and the partner-partial loads, so that its key
     // loads land during those waits (B = 1: 1.69 -> 1.65 ms, B = 1024: -1 %)
     V6_STAMP(3);
@@ -194,7 +210,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     // waits lgkmcnt(0) per pair, or per post-twist twiddle, i.e. one LDS round trip each.
     {
         Cx o[8];
+#ifdef TFHE_AMD_DIAG_NOHAND
+#pragma unroll
+        for (int r = 0; r < 8; ++r) o[r] = Y[r];
+#else
         load_C(sh.X[1 - w], o, L);
+#endif
         SCHED_FENCE();
         mac6(D, bv, Y);
 #pragma unroll
@@ -204,7 +225,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
         }
     }
     pass_dit_C(Y);
-    const Tw4 tB = tw7_invB(sh.tw, L);
+    const Tw4 tB = TW7(tw7_invB);
     V6_STAMP(5);
     lds_barrier6();   // the other wave has read X[w]
     V6_STAMP(6);
@@ -214,10 +235,17 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     SCHED_FENCE();
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
-        const Tw4 tI = tw7_invA(sh.tw, L);
+        const Tw4 tI = TW7(tw7_invA);
         Cx z[8];                                 // post-twist zeta^-n, n = L + 64 r
+#ifdef TFHE_AMD_DIAG_NOTW
+        {
+            const Tw4 d = diag_tw(L);
+            z[0] = d.w0; z[1] = d.w1; z[2] = d.w2a; z[3] = d.w2b; z[4] = d.w1; z[5] = d.w0; z[6] = d.w2b; z[7] = d.w2a;
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 8; ++r) z[r] = ld(sh.tw + kT7Post + r * 64 + L);
+#endif
 #ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
         store_B_ab(X, Y, L);
@@ -238,8 +266,8 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     // rounding distance for the exactness guard
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        acc[r] += torus_of_chk(Y[r].re, mx);
-        acc[r + 8] += torus_of_chk(Y[r].im, mx);
+        acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
+        acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
     }
     wave_sync();
     V6_STAMP(8);
@@ -290,6 +318,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
 #endif
     const int prio = g.prio;
     double mx = 0.0;                     // largest rounding distance of this lane (guard)
+    uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;   // range of the rounding shifter's high word (guard)
     int a_next = sh.bara[0];
     for (int i = 0; i < kn; ++i) {
         const int a = a_next;
@@ -304,9 +333,10 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc, mx V6_STAMPS_ARG);
+        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
     }
     if (g.flags) {   // exactness guard: this wave's largest rounding distance (high word)
+        if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
         const uint32_t h = wave_max_hi(mx);
         if (L == 0) {
             g.flags[2 * slot + w] = h;
@@ -402,7 +432,8 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         V6Stamps stamps;
 #endif
         double mx = 0.0;
-        cmux_v6<2>(sh, g, tA, i, a, w, L, ac, mx V6_STAMPS_ARG);
+        uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
+        cmux_v6<2>(sh, g, tA, i, a, w, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];

@@ -272,17 +272,27 @@ __device__ __forceinline__ uint32_t torus_of(double c) {
     return (uint32_t)__double_as_longlong(y);
 }
 
-// the same, and mx = max(mx, |c - rint(c)|): q = t + y = k + rint(c - k) is exact (|c| < 2^52),
-// and so is c - q (Fast2Sum error of y; Sterbenz) — the exactness guard's measurement, 2 fp64
-// adds and one max per coefficient (TFHE_AMD_V6_NOGUARD: A/B builds without it)
-__device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx) {
-    constexpr double M1 = 0x1.8p84, M12 = 0x1.8p84 + 0x1.8p52;
-    const double s = c + M1;
-    const double t = s - M12;
-    const double y = c - t;
+// rint(c) mod 2^32 with the exactness guard's measurement, in one shifter: y = c + 1.5 * 2^52.
+// For |c| < 2^51, y lies in [2^52, 2^53) (ulp 1), so y rounds c to the nearest integer and the
+// low mantissa word is rint(c) mod 2^32; q = y - 1.5 * 2^52 and c - q are exact, and
+// mx = max(mx, |c - q|) is the rounding distance.  Outside that range (the product bound is
+// |c| <= 2^52; real keys give < 2^48) y's exponent differs and its low word is not rint(c):
+// the high word of y, tracked as hlo = min and hhi = max, must stay in [0x43300000, 0x43400000)
+// or the kernel flags the ciphertext (tests/test_guard.py emulates exactly these operations).
+// 3 fp64 adds, one fp64 max and two integer min / max per coefficient (the previous form: two
+// shifters plus a Fast2Sum error, 5 fp64 ops and a max).  TFHE_AMD_V6_NOGUARD: the shifter
+// alone (A/B builds; exact only while |c| < 2^51).
+constexpr uint32_t kShiftHiLo = 0x43300000u;   // high word of 2^52
+constexpr uint32_t kShiftHiEnd = 0x43400000u;  // high word of 2^53
+__device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx, uint32_t &hlo, uint32_t &hhi) {
+    constexpr double M2 = 0x1.8p52;
+    const double y = c + M2;
 #ifndef TFHE_AMD_V6_NOGUARD
-    const double q = t + y;
+    const double q = y - M2;
     mx = __builtin_fmax(mx, __builtin_fabs(c - q));
+    const uint32_t hy = (uint32_t)((unsigned long long)__double_as_longlong(y) >> 32);
+    hlo = hy < hlo ? hy : hlo;
+    hhi = hy > hhi ? hy : hhi;
 #endif
     return (uint32_t)__double_as_longlong(y);
 }

@@ -119,3 +119,37 @@ def test_guard_catches_worst_case_key(keyset, rng):
     want = O.OracleKey(bk, keyset.ksk).woks_batch(T.MU, x_a, x_b)
     assert dist >= 0.25 and redo == B, (dist, redo)
     assert np.array_equal(u[0], want[0]) and np.array_equal(u[1], want[1])
+
+
+def _torus_of_chk(c):
+    """numpy restatement of csrc/fft_wave.h torus_of_chk (IEEE double, the kernel's ops):
+    returns (low word of y, rounding distance |c - q|, high word of y)."""
+    c = np.asarray(c, dtype=np.float64)
+    M2 = np.float64(1.5 * 2.0**52)
+    y = c + M2
+    q = y - M2
+    bits = y.view(np.uint64)
+    return (bits & 0xFFFFFFFF).astype(np.uint32), np.abs(c - q), (bits >> 32).astype(np.uint32)
+
+
+def test_single_shifter_rounding_exact_or_flagged():
+    """The kernel's mod-2^32 rounding (one 1.5 * 2^52 shifter) is exact for |c| < 2^51 and, over
+    the whole product range |c| <= 2^52, either exact or flagged by the guard (distance >= 1/4,
+    or the shifter's high word outside [hi(2^52), hi(2^53)), i.e. |c| >= 2^51)."""
+    r = np.random.default_rng(9)
+    mags = np.concatenate([r.uniform(-2.0**47, 2.0**47, 20000),
+                           r.uniform(-2.0**52, 2.0**52, 20000),
+                           r.uniform(2.0**50, 2.0**52, 5000) * r.choice([-1, 1], 5000)])
+    fr = r.uniform(-0.49, 0.49, mags.shape)
+    ints = np.floor(mags)
+    c = ints + fr                                       # representable up to the ulp
+    edges = np.array([2.0**51 - 1, 2.0**51, 2.0**51 + 1, 2.0**51 + 0.5, -2.0**51, -2.0**51 - 1,
+                      -2.0**51 - 0.5, 2.0**52, -2.0**52, 2.0**52 - 1, 0.49, -0.49, 0.0, 2.0**31])
+    c = np.concatenate([c, edges])
+    low, dist, hy = _torus_of_chk(c)
+    want = (np.vectorize(lambda v: int(np.rint(v)) % 2**32)(c)).astype(np.uint32)
+    flagged = (dist >= 0.25) | (hy < 0x43300000) | (hy >= 0x43400000)
+    assert np.array_equal(low[~flagged], want[~flagged])
+    small = np.abs(c) < 2.0**51
+    assert not flagged[small & (np.abs(c - np.rint(c)) < 0.25)].any()
+    assert flagged[(c == -2.0**51 - 1) | (c == 2.0**51 + 1) | (c == 2.0**52)].all()   # the high-word checks
