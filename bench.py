@@ -20,7 +20,9 @@ Rank 0 prints ONE JSON line.  Extra objects:
                  algorithmic bytes (every ciphertext streaming the 32.768 MB key; the batch
                  shares each key slice through L2, so those are cache hits, not HBM reads).
                  `clock` = the shader clock sampled during a sustained run (amd-smi), and the
-                 fp64 fraction at that clock.
+                 fp64 fraction at that clock.  `sustained` = the fp64 FMA rate the chip holds
+                 under its power limit (tfhe_amd_fp64_ceiling: pure register FMA chains, at the
+                 kernel's 2 waves per SIMD and at 8) and the kernel's fraction of each.
   batches      : the same step at B = 1 and 4096 per GPU (BASELINE metric's other batch sizes)
   strong       : global batch 4096 split over the ranks (BASELINE: batch 4096 on 1..8 GPUs)
   cpu_baseline : the optimized CPU port (oracle/cpu_fft.c: fp64 FFT external product, the
@@ -66,6 +68,7 @@ def parse():
     ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the sustained fp64 ceiling measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     return ap.parse_args()
 
@@ -339,6 +342,20 @@ def main():
             held = FP64_PEAK_TFLOPS * clk["mhz"] / PEAK_CLOCK_MHZ
             roof["clock"] = {"gfx_mhz": clk["mhz"], "samples": clk["samples"],
                              "fp64_peak_at_clock": held, "frac_at_clock": roof["achieved"] / held}
+    # the fp64 rate the chip sustains under its power limit (tfhe_amd_fp64_ceiling: register-
+    # operand FMA chains on every SIMD), at the kernel's occupancy and at the best one
+    if not args.no_ceiling and fft:
+        ceil = {}
+        for wps in (2, 8):
+            tf, mhz = T.fp64_ceiling(local, wps, 2.0)
+            ceil[wps] = (tf, mhz)
+        roof["sustained"] = {
+            "tflops_at_occupancy": ceil[2][0], "mhz_at_occupancy": ceil[2][1], "waves_per_simd": 2,
+            "frac_at_occupancy": roof["achieved"] / ceil[2][0],
+            "tflops_best": ceil[8][0], "mhz_best": ceil[8][1], "frac_best": roof["achieved"] / ceil[8][0],
+            "note": "fp64 FMA chains on register operands on every SIMD for 2 s (no memory, no LDS): "
+                    "the rate the chip holds under its power limit; k_blind_rotate_v6 runs 2 waves "
+                    "per SIMD at B = 1024 (DESIGN.md 5.1)"}
     if world > 1:
         dist.barrier()
 

@@ -142,12 +142,20 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
 template <int WAVES>
-__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int L,
-                                        uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
-    double2 *X = sh.X[w];
+__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
+                                        int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
+    double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
+#ifdef TFHE_AMD_DIAG_SHAREBK
+    // timing diagnostic (wrong results): both waves read wave 0's key rows in wave 0's order, so
+    // the second reader of each line hits the CU's L1 (what sharing the key slice would save)
+    const double2 *bk = g.bk + (size_t)i * 8 * 512 + L;
+#define KEYC(c) ((c) ^ w)
+#else
     const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
+#define KEYC(c) (c)
+#endif
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
 #ifndef TFHE_AMD_DIAG_NOEXT   // timing diagnostic (wrong results): no accumulator-extension stores
     write_ext(E, acc, L);
@@ -190,12 +198,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     Cx Y[8];
     // (issuing them at the top of the step instead, in flight for the whole forward transform,
     // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
-    load_bk(bv, bk, 1 - w);
+    load_bk(bv, bk, KEYC(1 - w));
     __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
     fft_fwd_C<2>(D, tC);
     mac6(D, bv, Y);
     V6_STAMP(2);
-    load_bk(bv, bk, w);
+    load_bk(bv, bk, KEYC(w));
     __builtin_amdgcn_sched_barrier(0);
 #ifndef TFHE_AMD_DIAG_NOHAND   // timing diagnostic (wrong results): no partial-sum hand-off
     store_C(X, Y, L);
@@ -214,7 +222,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = Y[r];
 #else
-        load_C(sh.X[1 - w], o, L);
+        load_C(sh.X[1 - own], o, L);
 #endif
         SCHED_FENCE();
         mac6(D, bv, Y);
@@ -227,7 +235,12 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     pass_dit_C(Y);
     const Tw4 tB = TW7(tw7_invB);
     V6_STAMP(5);
-    lds_barrier6();   // the other wave has read X[w]
+    // Buffer hand-over instead of a second barrier: the wave goes on in the partner's buffer,
+    // which the partner has finished with (it wrote its partial sum there before the barrier and
+    // now works in ours); LDS runs this wave's reads of it before its stores.  The two waves swap
+    // buffers every step (B = 1024: one s_barrier per step instead of two).
+    X = sh.X[1 - own];
+    own = 1 - own;
     V6_STAMP(6);
     store_C(X, Y, L);
     wave_sync();
@@ -320,6 +333,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     double mx = 0.0;                     // largest rounding distance of this lane (guard)
     uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;   // range of the rounding shifter's high word (guard)
     int a_next = sh.bara[0];
+    int own = w;                         // this wave's LDS buffer (the waves swap every step)
     for (int i = 0; i < kn; ++i) {
         const int a = a_next;
         a_next = sh.bara[i + 1 < kn ? i + 1 : i];   // a step ahead: no LDS round trip at the loop head
@@ -333,7 +347,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES>(sh, g, tA, i, a, w, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<WAVES>(sh, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
     }
     if (g.flags) {   // exactness guard: this wave's largest rounding distance (high word)
         if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
@@ -347,7 +361,9 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     if (blockIdx.x == 0 && blockIdx.y == 0 && L == 0)
         for (int k = 0; k < 10; ++k) g_v6_stamps[w][k] += stamps.acc[k];
 #endif
-    // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
+    // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]; the other
+    // wave may still be in its last inverse in either buffer
+    __syncthreads();
     if (w == 0) {
         uint32_t *E = reinterpret_cast<uint32_t *>(sh.X[0]);
         write_ext(E, acc, L);
@@ -425,6 +441,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
     for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
+    int own = w;
     for (int i = 0; i < iters; ++i) {
         const int a = sh.bara[i];
         if (a == 0) continue;
@@ -433,8 +450,9 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #endif
         double mx = 0.0;
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
-        cmux_v6<2>(sh, g, tA, i, a, w, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<2>(sh, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
     }
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];
 }

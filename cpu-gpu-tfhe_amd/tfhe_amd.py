@@ -75,6 +75,7 @@ def _load():
     L.tfhe_amd_guard_stats.argtypes = [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                                        ctypes.c_int]
     L.tfhe_amd_set_guard_threshold.argtypes = [ctypes.c_double]
+    L.tfhe_amd_fp64_ceiling.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _VP, _VP]
     L.tfhe_amd_tier1_lane_count.argtypes = [_VP]
     L.tfhe_amd_context_key_bytes.restype = ctypes.c_longlong
     L.tfhe_amd_context_key_bytes.argtypes = [_VP]
@@ -130,6 +131,15 @@ def available_kernels():
     out = [v for v in range(1, 8) if lib.tfhe_amd_select_kernel(v) == 0]
     lib.tfhe_amd_select_kernel(int(cur) if cur.isdigit() else 0)
     return out
+
+
+def fp64_ceiling(device=0, waves_per_simd=2, seconds=2.0):
+    """tfhe_amd_fp64_ceiling: (TFLOP/s, MHz) of register-operand fp64 FMA chains on every SIMD
+    for ~seconds: the fp64 rate the device sustains under its power limit (bench roofline)."""
+    tf, mhz = ctypes.c_double(), ctypes.c_double()
+    _check(lib.tfhe_amd_fp64_ceiling(int(device), int(waves_per_simd), float(seconds), ctypes.byref(tf),
+                                     ctypes.byref(mhz)), "fp64_ceiling")
+    return tf.value, mhz.value
 
 
 def set_guard_threshold(distance):

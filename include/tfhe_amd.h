@@ -196,6 +196,12 @@ int tfhe_amd_set_guard_threshold(double distance);
 /* build tag, e.g. "tfhe_amd gfx950 fft64 br-v6 ks-v4" */
 const char *tfhe_amd_version(void);
 
+/* Measurement (not on the bootstrapping path): the fp64 FMA rate the device sustains under its
+ * power limit, for the roofline in bench.py.  Every SIMD runs `waves_per_simd` waves of
+ * independent register-operand v_fma_f64 chains for about `seconds` (<= 30); *tflops = FLOP/s
+ * / 1e12 (FMA = 2), *mhz = the shader clock held meanwhile.  0 on success. */
+int tfhe_amd_fp64_ceiling(int device, int waves_per_simd, double seconds, double *tflops, double *mhz);
+
 /* ---------------------------------------------------------------- circuits (§8(f) row 1)
  * A circuit is a DAG of gates over SSA wires (ids 0, 1, ... in creation order; every wire
  * is written once).  tfhe_amd_circuit_run_dev evaluates B independent instances: wires are

@@ -16,7 +16,7 @@ for n in "$@"; do
     *) lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so ;;
   esac
   log=gpurun_out/ab_${n}_${AB_BATCH:-1024}_$rep.log
-  TFHE_AMD_GUARD=$guard TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline --no-clock --extra-batches '' --strong-batch 0 > $log 2>&1
+  TFHE_AMD_GUARD=$guard TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline --no-clock --no-ceiling --extra-batches '' --strong-batch 0 > $log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; tail -5 $log; exit $rc; }
   python3 -c "
 import json,sys

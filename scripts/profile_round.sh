@@ -9,7 +9,7 @@ BATCH=${2:-1024}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --batch $BATCH --no-cpu-baseline --no-clock --extra-batches none --strong-batch 0"
+BENCH="$R/bench.py --steps 5 --warmup 1 --batch $BATCH --no-cpu-baseline --no-clock --no-ceiling --extra-batches none --strong-batch 0"
 run() {   # name, extra rocprofv3 args...
   local name=$1; shift
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
