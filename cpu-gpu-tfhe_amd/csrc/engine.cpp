@@ -192,6 +192,7 @@ static int free_key(DeviceKey &k) {
     if (k.tw4) (void)hipFree(k.tw4);
     if (k.ksk) (void)hipFree(k.ksk);
     if (k.ksk4) (void)hipFree(k.ksk4);
+    if (k.ksk5) (void)hipFree(k.ksk5);
     if (k.tables) (void)hipFree(k.tables);
     k = DeviceKey();
     return 0;
@@ -299,8 +300,15 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
                 }
         HIPCHK(hipMalloc(&c->key.ksk, sizeof(int32_t) * packed.size()));
         HIPCHK(hipMemcpy(c->key.ksk, packed.data(), sizeof(int32_t) * packed.size(), hipMemcpyHostToDevice));
-        HIPCHK(hipMalloc(&c->key.ksk4, sizeof(int32_t) * ksk_v4_words()));
-        HIPCHK(launch_ksk_to_v4(c->key.ksk, c->key.ksk4, c->stream));
+        // batches above the small-batch kernel's range: the int8 MFMA key switch (ks-v5) or,
+        // with TFHE_AMD_KS5=0, ks-v4; only the chosen layout is built
+        if (ks5_enabled()) {
+            HIPCHK(hipMalloc(&c->key.ksk5, sizeof(int32_t) * ksk_v5_words()));
+            HIPCHK(launch_ksk_to_v5(c->key.ksk, c->key.ksk5, c->stream));
+        } else {
+            HIPCHK(hipMalloc(&c->key.ksk4, sizeof(int32_t) * ksk_v4_words()));
+            HIPCHK(launch_ksk_to_v4(c->key.ksk, c->key.ksk4, c->stream));
+        }
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     return tfhe_amd_reserve(c, 64);
@@ -355,6 +363,7 @@ extern "C" long long tfhe_amd_context_key_bytes(const TfheAmdContext *c) {
     if (k.tw6) n += (long long)kTw6Words * 16;
     if (k.ksk) n += (long long)kN * kKsT * 3 * kKsRow * 4;
     if (k.ksk4) n += (long long)ksk_v4_words() * 4;
+    if (k.ksk5) n += (long long)ksk_v5_words() * 4;
     if (k.tables) n += (long long)sizeof(NttTables);
     return n;
 }
@@ -776,7 +785,7 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
 
 extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ, int B, int32_t *wires_a,
                                         int32_t *wires_b, void *stream) {
-    if (!c || !circ || B < 0 || !c->key.has_bk || !c->key.ksk4) return TFHE_AMD_E_ARG;
+    if (!c || !circ || B < 0 || !c->key.has_bk || !(c->key.ksk4 || c->key.ksk5)) return TFHE_AMD_E_ARG;
     if (B == 0) return TFHE_AMD_OK;
     if (!wires_a || !wires_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;

@@ -18,6 +18,7 @@ struct DeviceKey {
     double2 *tw6 = nullptr;       // v6 twiddles: forward [4] + [4][64] x 2, inverse [4][64] x 2, post-twist [8][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     int32_t *ksk4 = nullptr;      // ks-v4: [126 column blocks][kN][kKsT][3][4]
+    int32_t *ksk5 = nullptr;      // ks-v5 (int8 MFMA): [64 N-blocks][kN][64 lanes][16 B] signed key bytes
     NttTables *tables = nullptr;  // device copy
     uint32_t qinv_neg[2] = {0, 0};
     uint32_t crt_h = 0, crt_hp = 0;
@@ -154,6 +155,9 @@ hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, cons
 // which key-switch kernel runs: 1..4 (env TFHE_AMD_KS)
 int ks_version();
 size_t ksk_v4_words();
+size_t ksk_v5_words();
+bool ks5_enabled();   // env TFHE_AMD_KS5=0: ks-v4 instead of the int8 MFMA key switch
+hipError_t launch_ksk_to_v5(const int32_t *d_ksk, int32_t *d_ksk5, hipStream_t s);
 // circuit level key switch: nks outputs x B instances; lane t = g B + k
 hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const CircKs *ks, const int32_t *u_a,
                                  const int32_t *u_b, int32_t *wa, int32_t *wb, hipStream_t s);

@@ -427,6 +427,183 @@ __global__ __launch_bounds__(512) void k_keyswitch_small(const int32_t *__restri
     atomicAdd(reinterpret_cast<unsigned int *>(dst), acc);
 }
 
+// ---------------------------------------------------------------- v5: int8 MFMA product
+// The key switch is a product with a one-hot matrix: res = (0, b) - sum_{i, j} KS[i][j][a_ij],
+// a_ij = the j-th base-4 digit of u_i + 2^15 (lwe-keyswitch-functions.cu:101-127), is
+//   S[m][col] = sum_k A[m][k] W[k][col],  k = (i, j, h),  A[m][k] = [a_ij(m) = h],
+//   W[(i, j, h)][col] = KS[i][j][h][col]  (h = 0: the zero row, lwe-keyswitch-functions.cu:919)
+// over K = 1024 x 8 x 4 = 32 768.  W is int32; written as 4 balanced signed bytes
+// w = sum_b s_b 2^(8 b) mod 2^32 (s_b in [-128, 127]), S = sum_b 2^(8 b) (A W_b) mod 2^32, and
+// every A W_b is exact in int32 (|A W_b| <= 8 192 x 128).  So the key switch runs as
+// v_mfma_i32_32x32x32_i8 with no rounding anywhere: N = 512 columns (501 used) x 4 limbs,
+// interleaved n = 4 col + limb, in 64 N-blocks of 32.
+// One K-step (32) = one key index i: lane l (row r = l & 31, half h = l >> 5) gives A bytes
+// 16 h + 4 t + hh = [a_{i, 4h+t} = hh], i.e. dword t = 1 << (8 a_{i, 4h+t}); the four digits of a
+// lane are one byte x of u_i + 2^15, so the fragment is one 16-B read of a 256-entry LDS table.
+// Its B fragment (16 B at [nb][i][l], pre-arranged by k_ksk_to_v5) is staged per chunk of
+// kKs5Ch key indices in LDS and shared by the workgroup's kKs5Waves waves (32 ciphertexts each).
+// Operand / result lane maps checked with exact integer data (scripts/mfma_i8_map.hip).
+typedef int ks5_v4i __attribute__((ext_vector_type(4)));
+typedef int ks5_v16i __attribute__((ext_vector_type(16)));
+#ifndef TFHE_AMD_KS5_WAVES
+#define TFHE_AMD_KS5_WAVES 8
+#endif
+constexpr int kKs5Waves = TFHE_AMD_KS5_WAVES;   // M: 8 x 32 = 256 ciphertexts per workgroup
+constexpr int kKs5Threads = 64 * kKs5Waves;
+constexpr int kKs5Ch = 16;                      // key indices per LDS chunk (16 KB)
+constexpr int kKs5Nb = 64;                      // N-blocks: 8 columns x 4 limbs each
+constexpr int kKs5Cols = 8 * kKs5Nb;            // 512 >= 501
+static_assert(kKs5Cols > kn, "the N-blocks cover every column and b");
+constexpr int kKs5ChU4 = kKs5Ch * 64;           // uint4 per chunk
+static_assert(kKs5ChU4 % kKs5Threads == 0, "chunk must split evenly");
+constexpr int kKs5Pieces = kKs5ChU4 / kKs5Threads;
+#ifndef TFHE_AMD_KS5_G
+#define TFHE_AMD_KS5_G 8
+#endif
+constexpr int kKs5G = TFHE_AMD_KS5_G;          // fragment pairs read ahead of their MFMAs
+static_assert(kKs5Ch % kKs5G == 0, "groups split the chunk");
+
+template <class P>
+__global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__restrict__ w5, P io) {
+    __shared__ __attribute__((aligned(16))) uint4 lut[256];
+    __shared__ __attribute__((aligned(16))) uint4 bs[2][kKs5Ch][64];
+    // digit bytes of the workgroup's ciphertexts for one chunk: dg[buf][half][ct][ii] = bits
+    // 24 - 8 half .. 31 - 8 half of u_i + u2_i + 2^15, i = chunk * kKs5Ch + ii
+    __shared__ __attribute__((aligned(16))) uint8_t dg[2][2][32 * kKs5Waves][kKs5Ch];
+    // XCD-aware: the M-tiles of one N-block run on one XCD (blockIdx % 8), reading its B stream
+    // together through that XCD's L2
+    const int bid = (int)blockIdx.x, xcd = bid & 7, kk = bid >> 3;
+    const int nb = xcd + 8 * (kk & 7), mt = kk >> 3;
+    const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, r = l & 31, hh = l >> 5;
+    for (int x = tid; x < 256; x += kKs5Threads)
+        lut[x] = make_uint4(1u << (8 * ((x >> 6) & 3)), 1u << (8 * ((x >> 4) & 3)), 1u << (8 * ((x >> 2) & 3)),
+                            1u << (8 * (x & 3)));
+    // loader role: thread t fetches 8 of the kKs5Ch sample words of ciphertext t / 2 per chunk
+    // (rows past the batch read row 0: their results are never stored, rows are independent)
+    constexpr int kPer = kKs5Ch / 2;
+    static_assert(2 * 32 * kKs5Waves == kKs5Threads && kPer == 8, "loader mapping");
+    const int lct = tid >> 1, lpart = tid & 1;
+    const int lg = mt * (32 * kKs5Waves) + lct;
+    const KsLane lln = io.lane(lg < io.count() ? lg : 0);
+    const uint4 *pa = reinterpret_cast<const uint4 *>(lln.ua) + 2 * lpart;
+    const uint4 *pa2 = reinterpret_cast<const uint4 *>(lln.ua2 ? lln.ua2 : lln.ua) + 2 * lpart;
+    const uint32_t m2 = lln.ua2 ? 0xffffffffu : 0u;   // no second sample: add it masked to 0
+    uint4 u0 = pa[0], u1 = pa[1], v0 = pa2[0], v1 = pa2[1];
+    auto put_digits = [&](int buf) {
+        uint32_t w[kPer] = {u0.x + (v0.x & m2), u0.y + (v0.y & m2), u0.z + (v0.z & m2), u0.w + (v0.w & m2),
+                            u1.x + (v1.x & m2), u1.y + (v1.y & m2), u1.z + (v1.z & m2), u1.w + (v1.w & m2)};
+        uint32_t hi0 = 0, hi1 = 0, lo0 = 0, lo1 = 0;   // bytes 3 (half 0) and 2 (half 1), packed
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t a = w[q] + kKsPrecOffset, b = w[q + 4] + kKsPrecOffset;
+            hi0 |= (a >> 24) << (8 * q);
+            hi1 |= (b >> 24) << (8 * q);
+            lo0 |= ((a >> 16) & 255u) << (8 * q);
+            lo1 |= ((b >> 16) & 255u) << (8 * q);
+        }
+        *reinterpret_cast<uint2 *>(&dg[buf][0][lct][kPer * lpart]) = make_uint2(hi0, hi1);
+        *reinterpret_cast<uint2 *>(&dg[buf][1][lct][kPer * lpart]) = make_uint2(lo0, lo1);
+    };
+    const uint4 *src = w5 + (size_t)nb * kN * 64 + tid;
+    uint4 p[kKs5Pieces];
+#pragma unroll
+    for (int q = 0; q < kKs5Pieces; ++q) p[q] = src[q * kKs5Threads];
+#pragma unroll
+    for (int q = 0; q < kKs5Pieces; ++q) (&bs[0][0][0])[tid + q * kKs5Threads] = p[q];
+    put_digits(0);
+    __syncthreads();
+    ks5_v16i acc = {};
+    constexpr int kChunks = kN / kKs5Ch;
+    const int row = wave * 32 + r;
+    for (int c = 0; c < kChunks; ++c) {
+        const bool more = c + 1 < kChunks;
+        {   // next chunk in flight during this one (the last iteration reloads its own: harmless)
+            const int cn = more ? c + 1 : c;
+            const uint4 *sn = src + (size_t)cn * kKs5ChU4;
+#pragma unroll
+            for (int q = 0; q < kKs5Pieces; ++q) p[q] = sn[q * kKs5Threads];
+            u0 = pa[cn * (kKs5Ch / 4)];
+            u1 = pa[cn * (kKs5Ch / 4) + 1];
+            v0 = pa2[cn * (kKs5Ch / 4)];
+            v1 = pa2[cn * (kKs5Ch / 4) + 1];
+        }
+        const uint4 xd = *reinterpret_cast<const uint4 *>(&dg[c & 1][hh][row][0]);
+        const uint32_t xw[4] = {xd.x, xd.y, xd.z, xd.w};
+        const uint4(*cur)[64] = bs[c & 1];
+        // fragments read in groups of kKs5G (all reads of a group issued before its MFMAs)
+#pragma unroll
+        for (int g = 0; g < kKs5Ch; g += kKs5G) {
+            uint4 av[kKs5G], bv[kKs5G];
+#pragma unroll
+            for (int q = 0; q < kKs5G; ++q) {
+                const int ii = g + q;
+                av[q] = lut[(xw[ii >> 2] >> (8 * (ii & 3))) & 255u];
+                bv[q] = cur[ii][l];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep the group's reads ahead of its MFMAs
+#pragma unroll
+            for (int q = 0; q < kKs5G; ++q) {
+                const ks5_v4i a = {(int)av[q].x, (int)av[q].y, (int)av[q].z, (int)av[q].w};
+                const ks5_v4i b = {(int)bv[q].x, (int)bv[q].y, (int)bv[q].z, (int)bv[q].w};
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+            }
+        }
+        if (more) {                              // other buffers: every wave finished them a chunk ago
+#pragma unroll
+            for (int q = 0; q < kKs5Pieces; ++q) (&bs[(c + 1) & 1][0][0])[tid + q * kKs5Threads] = p[q];
+            put_digits((c + 1) & 1);
+        }
+        __syncthreads();
+    }
+    // limbs -> Torus32: lane l holds column nb * 8 + (l & 31) / 4, limb l & 3, and ciphertext rows
+    // (reg & 3) + 8 (reg >> 2) + 4 hh of the wave's 32; the quad of lanes 4 q .. 4 q + 3 sums
+    // its limbs shifted into place (wrapping: exact mod 2^32) and its first lane stores
+    const int col = nb * 8 + (r >> 2);
+    const uint32_t lsh = 8u * (uint32_t)(l & 3);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        uint32_t v = (uint32_t)acc[reg] << lsh;
+        v += (uint32_t)__shfl_xor((int)v, 1, 64);
+        v += (uint32_t)__shfl_xor((int)v, 2, 64);
+        const int ctm = mt * (32 * kKs5Waves) + wave * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
+        if ((l & 3) == 0 && ctm < io.count() && col <= kn) {
+            const KsLane lm = io.lane(ctm);
+            if (col < kn) lm.ra[col] = (int32_t)(0u - v);
+            else *lm.rb = (int32_t)(lm.b - v);
+        }
+    }
+}
+
+// raw KSK [i][j][h - 1][kKsRow] -> v5 B fragments [nb][i][lane][16 B]: byte 4 t + hh of lane l =
+// limb (l & 3) of KS[i][4 (l >> 5) + t][hh][nb * 8 + (l & 31) / 4] as a balanced signed byte
+// (0 for hh = 0 and for columns > 500)
+__global__ __launch_bounds__(256) void k_ksk_to_v5(const int32_t *__restrict__ ksk, uint4 *__restrict__ w5) {
+    const size_t total = (size_t)kKs5Nb * kN * 64;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+        const int l = (int)(t & 63);
+        const int i = (int)((t >> 6) % kN);
+        const int nb = (int)(t / ((size_t)kN * 64));
+        const int col = nb * 8 + ((l & 31) >> 2), limb = l & 3, h = l >> 5;
+        uint32_t w[4];
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+            uint32_t word = 0;
+            for (int hh = 1; hh < 4; ++hh) {
+                if (col > kn) break;
+                uint32_t v = (uint32_t)ksk[(((size_t)i * kKsT + 4 * h + tt) * 3 + (hh - 1)) * kKsRow + col];
+                int8_t sb = 0;
+                for (int b = 0; b <= limb; ++b) {          // balanced base-256 digits, low first
+                    sb = (int8_t)(v & 0xffu);
+                    v = (v - (uint32_t)(int32_t)sb) >> 8;
+                }
+                word |= (uint32_t)(uint8_t)sb << (8 * hh);
+            }
+            w[tt] = word;
+        }
+        w5[t] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 // packed KSK [i][j][h - 1][kKsRow] -> v4 [cb][i][j][h - 1][4 cols]
 __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ ksk, uint4 *__restrict__ ksk4) {
     const size_t pieces = (size_t)kKs4Blocks * kN * kKsT * 3;
@@ -450,8 +627,23 @@ static int ks_split_max() {
     }();
     return v;
 }
+// Key switches above the small-batch range run on the int8 MFMA kernel (ks-v5) whenever the
+// context built its key layout, which it does unless TFHE_AMD_KS5=0 (then ks-v4: A/B runs)
+bool ks5_enabled() {
+    static const bool v = [] {
+        const char *e = getenv("TFHE_AMD_KS5");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
 template <class P>
 static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io, hipStream_t s) {
+    if (key.ksk5) {
+        const int mtiles = (count + 32 * kKs5Waves - 1) / (32 * kKs5Waves);
+        hipLaunchKernelGGL(k_keyswitch_v5<P>, dim3(mtiles * kKs5Nb), dim3(kKs5Threads), 0, s,
+                           reinterpret_cast<const uint4 *>(key.ksk5), io);
+        return;
+    }
     if (count <= ks_split_max()) {
         hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
         hipLaunchKernelGGL((k_keyswitch_v4<P, 2>), dim3(2 * 128 * groups), dim3(kKs4Threads), 0, s,
@@ -516,6 +708,12 @@ __global__ __launch_bounds__(256) void k_circuit_linear(int B, int nlin, const C
 }
 
 size_t ksk_v4_words() { return (size_t)kKs4Blocks * kN * kKsT * 3 * 4; }
+size_t ksk_v5_words() { return (size_t)kKs5Nb * kN * 64 * 4; }
+
+hipError_t launch_ksk_to_v5(const int32_t *d_ksk, int32_t *d_ksk5, hipStream_t s) {
+    hipLaunchKernelGGL(k_ksk_to_v5, dim3(4096), dim3(256), 0, s, d_ksk, reinterpret_cast<uint4 *>(d_ksk5));
+    return hipGetLastError();
+}
 
 hipError_t launch_circuit_linear(int B, int nlin, const CircLin *lin, int32_t *wa, int32_t *wb, hipStream_t s) {
     if (B <= 0 || nlin <= 0) return hipSuccess;

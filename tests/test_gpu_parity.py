@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C ABI) vs the CPU oracle, Torus32 bit-exact
 (SURVEY.md §8(c) P1), plus decryption truth tables (P2)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -9,6 +10,7 @@ import oracle_ctypes as O
 import tfhe_amd as T
 
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 N, n = 1024, 500
 TRUTH = {
@@ -189,10 +191,11 @@ def test_empty_batch_is_a_no_op(ctx, keyset, rng):
     assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - x)
 
 
-@pytest.mark.parametrize("B", [1, 96, 97, 400, 768, 769])
+@pytest.mark.parametrize("B", [1, 96, 97, 255, 256, 257, 400, 768, 769])
 def test_keyswitch_paths_bit_exact(ctx, okey, rng, B):
-    """Each key-switch path (small batch <= 96 via per-key-index workgroups and atomic partials,
-    97..768 via the key-index split of ks-v4, > 768 plain ks-v4) at and around its threshold."""
+    """Each key-switch path at and around its threshold: small batch <= 96 (per-key-index
+    workgroups, atomic partials), above it the int8 MFMA key switch (ks-v5; 256 ciphertexts per
+    workgroup: ragged last tile at 255 / 257 / 400 / 769)."""
     u_a = rng.integers(-2**31, 2**31, (B, N), dtype=np.int64).astype(np.int32)
     u_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
     k_a, k_b = ctx.keyswitch_host(u_a, u_b)
@@ -277,7 +280,8 @@ def test_scratch_reuse_across_streams(ctx, okey, keyset, rng):
 def test_context_key_memory_and_init(keyset):
     """Product builds hold only the key domains their kernels read: the FFT-domain key (v6),
     the NTT-domain key (v4, the exactness guard's fallback) and the two key-switching layouts
-    (ks-v4 and the small-batch kernel's) — about 166 MB per cloud key and GPU."""
+    (the int8 MFMA key switch's signed key bytes, 67 MB, and the small-batch kernel's rows) —
+    about 182 MB per cloud key and GPU."""
     import time
     t0 = time.perf_counter()
     c = T.Context(keyset.bk, keyset.ksk, device=0)
@@ -287,4 +291,28 @@ def test_context_key_memory_and_init(keyset):
     c.close()
     print(f"context init {init_s * 1e3:.0f} ms, key material {kb / 1e6:.1f} MB")
     if 1 not in T.available_kernels():      # product build
-        assert kb < 170e6, kb
+        assert kb < 185e6, kb
+
+
+def test_keyswitch_v4_layout_subprocess():
+    """TFHE_AMD_KS5=0 (read once per process) builds the ks-v4 layout instead of the MFMA key
+    switch's: that path, key-index split (<= 768) and plain, still equals the oracle."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np
+sys.path[:0] = [%r, %r]
+import tfhe_amd as T, oracle_ctypes as O
+K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); o = O.OracleKey(K.bk, K.ksk)
+rng = np.random.default_rng(3)
+for B in (400, 769):
+    u_a = rng.integers(-2**31, 2**31, (B, 1024), dtype=np.int64).astype(np.int32)
+    u_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    k_a, k_b = c.keyswitch_host(u_a, u_b); o_a, o_b = o.keyswitch_batch(u_a, u_b)
+    assert np.array_equal(k_a, o_a) and np.array_equal(k_b, o_b), B
+print("ks-v4 ok", c.key_bytes())
+""" % (os.path.join(REPO, "cpu-gpu-tfhe_amd"), os.path.join(REPO, "tests"))
+    env = dict(os.environ, TFHE_AMD_KS5="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ks-v4 ok" in r.stdout
