@@ -439,7 +439,7 @@ __global__ __launch_bounds__(512) void k_keyswitch_small(const int32_t *__restri
 // interleaved n = 4 col + limb, in 64 N-blocks of 32.
 // One K-step (32) = one key index i: lane l (row r = l & 31, half h = l >> 5) gives A bytes
 // 16 h + 4 t + hh = [a_{i, 4h+t} = hh], i.e. dword t = 1 << (8 a_{i, 4h+t}); the four digits of a
-// lane are one byte x of u_i + 2^15, so the fragment is one 16-B read of a 256-entry LDS table.
+// lane are one byte x of u_i + 2^15, so the fragment is two 8-B reads of a 16-entry (2-digit) LDS table.
 // Its B fragment (16 B at [nb][i][l], pre-arranged by k_ksk_to_v5) is staged per chunk of
 // kKs5Ch key indices in LDS and shared by the workgroup's kKs5Waves waves (32 ciphertexts each).
 // Operand / result lane maps checked with exact integer data (scripts/mfma_i8_map.hip).
@@ -465,7 +465,10 @@ static_assert(kKs5Ch % kKs5G == 0, "groups split the chunk");
 
 template <class P>
 __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__restrict__ w5, P io) {
-    __shared__ __attribute__((aligned(16))) uint4 lut[256];
+    // one-hot table per 2-digit nibble, one copy per lane of a 32-lane group: lane L reads entry
+    // n at [n][L & 31] (8 B), so every ds_read_b64 of a wave is bank-conflict free whatever the
+    // digits (a single 256-entry table read with b128 collided on random digits)
+    __shared__ __attribute__((aligned(16))) uint2 lut[16][32];
     __shared__ __attribute__((aligned(16))) uint4 bs[2][kKs5Ch][64];
     // digit bytes of the workgroup's ciphertexts for one chunk: dg[buf][half][ct][ii] = bits
     // 24 - 8 half .. 31 - 8 half of u_i + u2_i + 2^15, i = chunk * kKs5Ch + ii
@@ -475,9 +478,8 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     const int bid = (int)blockIdx.x, xcd = bid & 7, kk = bid >> 3;
     const int nb = xcd + 8 * (kk & 7), mt = kk >> 3;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, r = l & 31, hh = l >> 5;
-    for (int x = tid; x < 256; x += kKs5Threads)
-        lut[x] = make_uint4(1u << (8 * ((x >> 6) & 3)), 1u << (8 * ((x >> 4) & 3)), 1u << (8 * ((x >> 2) & 3)),
-                            1u << (8 * (x & 3)));
+    for (int e = tid; e < 16 * 32; e += kKs5Threads)
+        lut[e >> 5][e & 31] = make_uint2(1u << (8 * ((e >> 7) & 3)), 1u << (8 * ((e >> 5) & 3)));
     // loader role: thread t fetches 8 of the kKs5Ch sample words of ciphertext t / 2 per chunk
     // (rows past the batch read row 0: their results are never stored, rows are independent)
     constexpr int kPer = kKs5Ch / 2;
@@ -537,7 +539,9 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
 #pragma unroll
             for (int q = 0; q < kKs5G; ++q) {
                 const int ii = g + q;
-                av[q] = lut[(xw[ii >> 2] >> (8 * (ii & 3))) & 255u];
+                const uint32_t xb = xw[ii >> 2] >> (8 * (ii & 3));   // digits a_{4hh..4hh+3}, high first
+                const uint2 d01 = lut[(xb >> 4) & 15u][r], d23 = lut[xb & 15u][r];
+                av[q] = make_uint4(d01.x, d01.y, d23.x, d23.y);
                 bv[q] = cur[ii][l];
             }
             __builtin_amdgcn_sched_barrier(0);   // keep the group's reads ahead of its MFMAs

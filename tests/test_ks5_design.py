@@ -1,6 +1,6 @@
 """The int8-MFMA key switch (ks-v5, keyswitch.hip) checked on the CPU: a numpy restatement of its
 data flow — the balanced signed-byte split of the key (k_ksk_to_v5), the one-hot A fragments
-from the 256-entry digit table, the lane maps of v_mfma_i32_32x32x32_i8 (lane l = 32 h + r holds
+from the 2-digit (nibble) table, the lane maps of v_mfma_i32_32x32x32_i8 (lane l = 32 h + r holds
 A[r][16 h + j] and B[16 h + j][r] in byte j; checked on the GPU by scripts/mfma_i8_map.hip), the
 int32 sums per limb and their recombination mod 2^32 — against the oracle's key switch
 (lwe-keyswitch-functions.cu:101-127).  The GPU kernel itself is compared with the oracle in
@@ -42,14 +42,16 @@ def b_matrix(ksk):
 
 def a_matrix(u_a):
     """one-hot rows: A[m][32 i + 4 j + hh] = [digit j of u_i + 2^15 = hh], built the kernel's
-    way — one byte x per (i, lane half h), dword t of the table entry = 1 << (8 a_t)."""
+    way — one byte x per (i, lane half h), each nibble of it (2 digits) one table entry of two
+    dwords, dword t of the fragment = 1 << (8 a_t)."""
     M = u_a.shape[0]
     u = (u_a.astype(np.int64) + PREC) & 0xFFFFFFFF
     A = np.zeros((M, N, 2, 4, BASE), np.int64)
-    lut = np.zeros((256, 4, BASE), np.int64)
-    for x in range(256):
-        for t in range(4):
-            lut[x, t, (x >> (6 - 2 * t)) & 3] = 1
+    nib = np.zeros((16, 2, BASE), np.int64)          # the kernel's lut[n]: (1 << 8 (n >> 2), 1 << 8 (n & 3))
+    for n in range(16):
+        nib[n, 0, (n >> 2) & 3] = 1
+        nib[n, 1, n & 3] = 1
+    lut = np.concatenate([nib[np.arange(256) >> 4], nib[np.arange(256) & 15]], axis=1)   # [x][t][hh]
     for h in range(2):
         x = (u >> (24 - 8 * h)) & 255
         A[:, :, h] = lut[x]
