@@ -827,11 +827,11 @@ extern "C" int tfhe_amd_select_kernel(int br_version) {
 
 extern "C" const char *tfhe_amd_version(void) {
     // one immutable string per (blind-rotation, key-switch) generation pair
-    static char names[8][5][48];
+    static char names[8][6][48];
     static std::once_flag once;
     std::call_once(once, [] {
         for (int b = 0; b <= 7; b++)
-            for (int k = 1; k <= 4; k++) {
+            for (int k = 1; k <= 5; k++) {
                 if (b == 0 || b >= 6)
                     snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v%d ks-v%d", b == 7 ? 7 : 6, k);
                 else snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);

@@ -732,15 +732,17 @@ hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s
     return hipGetLastError();
 }
 
+// key-switch generation for batches above the small-batch range: 5 (int8 MFMA, the default),
+// 4 (TFHE_AMD_KS5=0), 1..3 (TFHE_AMD_KS, EXPERIMENTAL=1 builds)
 int ks_version() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_KS");
         const int x = e ? atoi(e) : 4;
 #ifdef TFHE_AMD_EXPERIMENTAL
-        return (x >= 1 && x <= 4) ? x : 4;
-#else
-        return x == 4 ? x : 4;   // ks-v1 .. v3 are in EXPERIMENTAL=1 builds only
+        if (x >= 1 && x <= 3) return x;
 #endif
+        (void)x;   // ks-v1 .. v3 are in EXPERIMENTAL=1 builds only
+        return ks5_enabled() ? 5 : 4;
     }();
     return v;
 }
