@@ -463,7 +463,10 @@ constexpr int kKs5Pieces = kKs5ChU4 / kKs5Threads;
 constexpr int kKs5G = TFHE_AMD_KS5_G;          // fragment pairs read ahead of their MFMAs
 static_assert(kKs5Ch % kKs5G == 0, "groups split the chunk");
 
-template <class P>
+// SPLIT > 1: the key indices are split over SPLIT workgroups per (N-block, M-tile), each adds its
+// partial sums (wrapping, exact in any order) into result rows zeroed (and given b) by
+// k_keyswitch_small_init — more workgroups for batches that give fewer than 2 per CU.
+template <class P, int SPLIT>
 __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__restrict__ w5, P io) {
     // one-hot table per 2-digit nibble, one copy per lane of a 32-lane group: lane L reads entry
     // n at [n][L & 31] (8 B), so every ds_read_b64 of a wave is bank-conflict free whatever the
@@ -476,7 +479,9 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     // XCD-aware: the M-tiles of one N-block run on one XCD (blockIdx % 8), reading its B stream
     // together through that XCD's L2
     const int bid = (int)blockIdx.x, xcd = bid & 7, kk = bid >> 3;
-    const int nb = xcd + 8 * (kk & 7), mt = kk >> 3;
+    const int nb = xcd + 8 * (kk & 7), part = (kk >> 3) % SPLIT, mt = (kk >> 3) / SPLIT;
+    constexpr int kChunks = kN / kKs5Ch / SPLIT;   // chunks of this workgroup's key-index range
+    const int c0 = part * kChunks;
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, r = l & 31, hh = l >> 5;
     for (int e = tid; e < 16 * 32; e += kKs5Threads)
         lut[e >> 5][e & 31] = make_uint2(1u << (8 * ((e >> 7) & 3)), 1u << (8 * ((e >> 5) & 3)));
@@ -490,7 +495,8 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     const uint4 *pa = reinterpret_cast<const uint4 *>(lln.ua) + 2 * lpart;
     const uint4 *pa2 = reinterpret_cast<const uint4 *>(lln.ua2 ? lln.ua2 : lln.ua) + 2 * lpart;
     const uint32_t m2 = lln.ua2 ? 0xffffffffu : 0u;   // no second sample: add it masked to 0
-    uint4 u0 = pa[0], u1 = pa[1], v0 = pa2[0], v1 = pa2[1];
+    uint4 u0 = pa[c0 * (kKs5Ch / 4)], u1 = pa[c0 * (kKs5Ch / 4) + 1];
+    uint4 v0 = pa2[c0 * (kKs5Ch / 4)], v1 = pa2[c0 * (kKs5Ch / 4) + 1];
     auto put_digits = [&](int buf) {
         uint32_t w[kPer] = {u0.x + (v0.x & m2), u0.y + (v0.y & m2), u0.z + (v0.z & m2), u0.w + (v0.w & m2),
                             u1.x + (v1.x & m2), u1.y + (v1.y & m2), u1.z + (v1.z & m2), u1.w + (v1.w & m2)};
@@ -506,7 +512,9 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
         *reinterpret_cast<uint2 *>(&dg[buf][0][lct][kPer * lpart]) = make_uint2(hi0, hi1);
         *reinterpret_cast<uint2 *>(&dg[buf][1][lct][kPer * lpart]) = make_uint2(lo0, lo1);
     };
-    const uint4 *src = w5 + (size_t)nb * kN * 64 + tid;
+    const uint4 *src = w5 + ((size_t)nb * kN + (size_t)c0 * kKs5Ch) * 64 + tid;
+    pa += c0 * (kKs5Ch / 4);
+    pa2 += c0 * (kKs5Ch / 4);
     uint4 p[kKs5Pieces];
 #pragma unroll
     for (int q = 0; q < kKs5Pieces; ++q) p[q] = src[q * kKs5Threads];
@@ -515,7 +523,6 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     put_digits(0);
     __syncthreads();
     ks5_v16i acc = {};
-    constexpr int kChunks = kN / kKs5Ch;
     const int row = wave * 32 + r;
     for (int c = 0; c < kChunks; ++c) {
         const bool more = c + 1 < kChunks;
@@ -572,7 +579,8 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
         const int ctm = mt * (32 * kKs5Waves) + wave * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
         if ((l & 3) == 0 && ctm < io.count() && col <= kn) {
             const KsLane lm = io.lane(ctm);
-            if (col < kn) lm.ra[col] = (int32_t)(0u - v);
+            if (SPLIT > 1) atomicAdd(reinterpret_cast<unsigned int *>(col < kn ? lm.ra + col : lm.rb), 0u - v);
+            else if (col < kn) lm.ra[col] = (int32_t)(0u - v);
             else *lm.rb = (int32_t)(lm.b - v);
         }
     }
@@ -640,12 +648,33 @@ bool ks5_enabled() {
     }();
     return v;
 }
+// key-index split of ks-v5: enough workgroups for about 2 per CU (512 for 256 CUs) when the
+// batch has few M-tiles (TFHE_AMD_KS5_SPLIT = 1, 2, 4 or 8 forces one)
+static int ks5_split(int mtiles) {
+    static const int forced = [] {
+        const char *e = getenv("TFHE_AMD_KS5_SPLIT");
+        const int v = e ? atoi(e) : 0;
+        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+    }();
+    if (forced) return forced;
+    int sp = 1;
+    while (sp < 8 && mtiles * kKs5Nb * sp < 512) sp *= 2;
+    return sp;
+}
 template <class P>
 static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io, hipStream_t s) {
     if (key.ksk5) {
         const int mtiles = (count + 32 * kKs5Waves - 1) / (32 * kKs5Waves);
-        hipLaunchKernelGGL(k_keyswitch_v5<P>, dim3(mtiles * kKs5Nb), dim3(kKs5Threads), 0, s,
-                           reinterpret_cast<const uint4 *>(key.ksk5), io);
+        const uint4 *w5 = reinterpret_cast<const uint4 *>(key.ksk5);
+        const int split = ks5_split(mtiles);
+        if (split > 1) hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
+        const dim3 grid(mtiles * kKs5Nb * split);
+        switch (split) {
+        case 8: hipLaunchKernelGGL((k_keyswitch_v5<P, 8>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+        case 4: hipLaunchKernelGGL((k_keyswitch_v5<P, 4>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+        case 2: hipLaunchKernelGGL((k_keyswitch_v5<P, 2>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+        default: hipLaunchKernelGGL((k_keyswitch_v5<P, 1>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+        }
         return;
     }
     if (count <= ks_split_max()) {
@@ -672,7 +701,9 @@ static int ks_unroll_max() {
 static int ks_small_max() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_KS_SMALL");
-        return e ? atoi(e) : 96;   // crossover with ks-v4 measured between 64 and 128
+        // crossover with ks-v5 (split 8: 0.036 ms flat up to 256) between 12 and 16 (B = 16:
+        // 0.039 vs 0.036 ms, B = 1: 0.021 vs 0.036); with ks-v4 (TFHE_AMD_KS5=0) between 64 and 128
+        return e ? atoi(e) : (ks5_enabled() ? 12 : 96);
     }();
     return v;
 }

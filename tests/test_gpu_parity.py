@@ -191,11 +191,12 @@ def test_empty_batch_is_a_no_op(ctx, keyset, rng):
     assert np.array_equal(keyset.decrypt(r_a, r_b), 1 - x)
 
 
-@pytest.mark.parametrize("B", [1, 96, 97, 255, 256, 257, 400, 768, 769])
+@pytest.mark.parametrize("B", [1, 12, 13, 96, 255, 256, 257, 400, 768, 769, 1025])
 def test_keyswitch_paths_bit_exact(ctx, okey, rng, B):
-    """Each key-switch path at and around its threshold: small batch <= 96 (per-key-index
+    """Each key-switch path at and around its threshold: small batch <= 12 (per-key-index
     workgroups, atomic partials), above it the int8 MFMA key switch (ks-v5; 256 ciphertexts per
-    workgroup: ragged last tile at 255 / 257 / 400 / 769)."""
+    workgroup: ragged last tile at 13 / 255 / 257 / 400 / 769 / 1025; key-index split 8 up to
+    256, 4 up to 512, 2 up to 1024, none above)."""
     u_a = rng.integers(-2**31, 2**31, (B, N), dtype=np.int64).astype(np.int32)
     u_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
     k_a, k_b = ctx.keyswitch_host(u_a, u_b)
