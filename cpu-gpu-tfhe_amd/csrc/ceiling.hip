@@ -51,9 +51,13 @@ __global__ __launch_bounds__(kCeilThreads) void k_fp64_ceiling(double *__restric
 // CU over it (s_memtime / s_memrealtime at 100 MHz).  0 on success.
 extern "C" int tfhe_amd_fp64_ceiling(int device, int waves_per_simd, double seconds, double *tflops, double *mhz) {
     if (!tflops || !mhz || waves_per_simd < 1 || waves_per_simd > 8 || !(seconds > 0.0) || seconds > 30.0) return -1;
-    if (hipSetDevice(device) != hipSuccess) return -2;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return -2;
     int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return -2;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) {
+        (void)hipSetDevice(prev);
+        return -2;
+    }
     // 4 waves per workgroup, one per SIMD: waves_per_simd workgroups per CU
     const int blocks = cus * waves_per_simd;
     double *out = nullptr;
@@ -90,5 +94,6 @@ done:
     if (e1) (void)hipEventDestroy(e1);
     if (out) (void)hipFree(out);
     if (clk) (void)hipFree(clk);
+    (void)hipSetDevice(prev);   // the caller's current device is left as it was
     return rc;
 }
