@@ -317,3 +317,16 @@ print("ks-v4 ok", c.key_bytes())
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ks-v4 ok" in r.stdout
+
+
+def test_fp64_ceiling_measurement():
+    """tfhe_amd_fp64_ceiling (bench.py's roofline.sustained): a plausible fp64 rate and clock, and
+    the caller's current device left as it was."""
+    torch = _torch()
+    dev = torch.cuda.current_device()
+    tf, mhz = T.fp64_ceiling(0, 2, 0.2)
+    assert 10.0 < tf < 80.0, tf          # MI355X fp64 vector peak 78.6 TFLOP/s
+    assert 500.0 < mhz < 2600.0, mhz
+    assert torch.cuda.current_device() == dev
+    with pytest.raises(T.TfheAmdError):
+        T.fp64_ceiling(0, 0, 1.0)
