@@ -461,13 +461,16 @@ constexpr int kKs5Pieces = kKs5ChU4 / kKs5Threads;
 #define TFHE_AMD_KS5_G 8
 #endif
 constexpr int kKs5G = TFHE_AMD_KS5_G;          // fragment pairs read ahead of their MFMAs
-static_assert(kKs5Ch % kKs5G == 0, "groups split the chunk");
 
 // SPLIT > 1: the key indices are split over SPLIT workgroups per (N-block, M-tile), each adds its
 // partial sums (wrapping, exact in any order) into result rows zeroed (and given b) by
 // k_keyswitch_small_init — more workgroups for batches that give fewer than 2 per CU.
-template <class P, int SPLIT>
+// MS: 32-ciphertext M-slices per wave sharing each B fragment read (1 or 2).
+template <class P, int SPLIT, int MS>
 __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__restrict__ w5, P io) {
+    constexpr int kM = 32 * kKs5Waves * MS;           // ciphertexts per workgroup (M-tile)
+    constexpr int kG = kKs5G / MS;                     // i-steps per read group
+    static_assert(kKs5Ch % kG == 0, "groups split the chunk");
     // one-hot table per 2-digit nibble, one copy per lane of a 32-lane group: lane L reads entry
     // n at [n][L & 31] (8 B), so every ds_read_b64 of a wave is bank-conflict free whatever the
     // digits (a single 256-entry table read with b128 collided on random digits)
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     __shared__ __attribute__((aligned(16))) uint4 bs[2][kKs5Ch][64];
     // digit bytes of the workgroup's ciphertexts for one chunk: dg[buf][half][ct][ii] = bits
     // 24 - 8 half .. 31 - 8 half of u_i + u2_i + 2^15, i = chunk * kKs5Ch + ii
-    __shared__ __attribute__((aligned(16))) uint8_t dg[2][2][32 * kKs5Waves][kKs5Ch];
+    __shared__ __attribute__((aligned(16))) uint8_t dg[2][2][kM][kKs5Ch];
     // XCD-aware: the M-tiles of one N-block run on one XCD (blockIdx % 8), reading its B stream
     // together through that XCD's L2
     const int bid = (int)blockIdx.x, xcd = bid & 7, kk = bid >> 3;
@@ -485,36 +488,44 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, r = l & 31, hh = l >> 5;
     for (int e = tid; e < 16 * 32; e += kKs5Threads)
         lut[e >> 5][e & 31] = make_uint2(1u << (8 * ((e >> 7) & 3)), 1u << (8 * ((e >> 5) & 3)));
-    // loader role: thread t fetches 8 of the kKs5Ch sample words of ciphertext t / 2 per chunk
-    // (rows past the batch read row 0: their results are never stored, rows are independent)
-    constexpr int kPer = kKs5Ch / 2;
-    static_assert(2 * 32 * kKs5Waves == kKs5Threads && kPer == 8, "loader mapping");
-    const int lct = tid >> 1, lpart = tid & 1;
-    const int lg = mt * (32 * kKs5Waves) + lct;
+    // loader role: thread t fetches kPer of the kKs5Ch sample words of ciphertext (t MS) / 2 per
+    // chunk (rows past the batch read row 0: their results are never stored, rows are independent)
+    constexpr int kPer = kKs5Ch * MS / 2;          // 8 or 16 words: 2 or 4 uint4
+    constexpr int kU4 = kPer / 4;
+    static_assert(kKs5Threads * kPer == kM * kKs5Ch, "loader mapping");
+    const int lct = (tid * MS) >> 1, lpart = MS == 1 ? (tid & 1) : 0;
+    const int lg = mt * kM + lct;
     const KsLane lln = io.lane(lg < io.count() ? lg : 0);
-    const uint4 *pa = reinterpret_cast<const uint4 *>(lln.ua) + 2 * lpart;
-    const uint4 *pa2 = reinterpret_cast<const uint4 *>(lln.ua2 ? lln.ua2 : lln.ua) + 2 * lpart;
+    const uint4 *pa = reinterpret_cast<const uint4 *>(lln.ua) + kU4 * lpart;
+    const uint4 *pa2 = reinterpret_cast<const uint4 *>(lln.ua2 ? lln.ua2 : lln.ua) + kU4 * lpart;
     const uint32_t m2 = lln.ua2 ? 0xffffffffu : 0u;   // no second sample: add it masked to 0
-    uint4 u0 = pa[c0 * (kKs5Ch / 4)], u1 = pa[c0 * (kKs5Ch / 4) + 1];
-    uint4 v0 = pa2[c0 * (kKs5Ch / 4)], v1 = pa2[c0 * (kKs5Ch / 4) + 1];
-    auto put_digits = [&](int buf) {
-        uint32_t w[kPer] = {u0.x + (v0.x & m2), u0.y + (v0.y & m2), u0.z + (v0.z & m2), u0.w + (v0.w & m2),
-                            u1.x + (v1.x & m2), u1.y + (v1.y & m2), u1.z + (v1.z & m2), u1.w + (v1.w & m2)};
-        uint32_t hi0 = 0, hi1 = 0, lo0 = 0, lo1 = 0;   // bytes 3 (half 0) and 2 (half 1), packed
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t a = w[q] + kKsPrecOffset, b = w[q + 4] + kKsPrecOffset;
-            hi0 |= (a >> 24) << (8 * q);
-            hi1 |= (b >> 24) << (8 * q);
-            lo0 |= ((a >> 16) & 255u) << (8 * q);
-            lo1 |= ((b >> 16) & 255u) << (8 * q);
-        }
-        *reinterpret_cast<uint2 *>(&dg[buf][0][lct][kPer * lpart]) = make_uint2(hi0, hi1);
-        *reinterpret_cast<uint2 *>(&dg[buf][1][lct][kPer * lpart]) = make_uint2(lo0, lo1);
-    };
-    const uint4 *src = w5 + ((size_t)nb * kN + (size_t)c0 * kKs5Ch) * 64 + tid;
     pa += c0 * (kKs5Ch / 4);
     pa2 += c0 * (kKs5Ch / 4);
+    uint4 uu[kU4], vv[kU4];
+#pragma unroll
+    for (int q = 0; q < kU4; ++q) {
+        uu[q] = pa[q];
+        vv[q] = pa2[q];
+    }
+    auto put_digits = [&](int buf) {
+        uint32_t hi[kPer / 4], lo[kPer / 4];   // bytes 3 (half 0) and 2 (half 1) of each word, packed
+#pragma unroll
+        for (int q = 0; q < kU4; ++q) {
+            const uint32_t w[4] = {uu[q].x + (vv[q].x & m2) + kKsPrecOffset, uu[q].y + (vv[q].y & m2) + kKsPrecOffset,
+                                   uu[q].z + (vv[q].z & m2) + kKsPrecOffset, uu[q].w + (vv[q].w & m2) + kKsPrecOffset};
+            hi[q] = (w[0] >> 24) | ((w[1] >> 24) << 8) | ((w[2] >> 24) << 16) | ((w[3] >> 24) << 24);
+            lo[q] = ((w[0] >> 16) & 255u) | (((w[1] >> 16) & 255u) << 8) | (((w[2] >> 16) & 255u) << 16) |
+                    (((w[3] >> 16) & 255u) << 24);
+        }
+        if (kU4 == 2) {
+            *reinterpret_cast<uint2 *>(&dg[buf][0][lct][kPer * lpart]) = make_uint2(hi[0], hi[1]);
+            *reinterpret_cast<uint2 *>(&dg[buf][1][lct][kPer * lpart]) = make_uint2(lo[0], lo[1]);
+        } else {
+            *reinterpret_cast<uint4 *>(&dg[buf][0][lct][0]) = make_uint4(hi[0], hi[1], hi[2 % kU4], hi[3 % kU4]);
+            *reinterpret_cast<uint4 *>(&dg[buf][1][lct][0]) = make_uint4(lo[0], lo[1], lo[2 % kU4], lo[3 % kU4]);
+        }
+    };
+    const uint4 *src = w5 + ((size_t)nb * kN + (size_t)c0 * kKs5Ch) * 64 + tid;
     uint4 p[kKs5Pieces];
 #pragma unroll
     for (int q = 0; q < kKs5Pieces; ++q) p[q] = src[q * kKs5Threads];
@@ -522,8 +533,9 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
     for (int q = 0; q < kKs5Pieces; ++q) (&bs[0][0][0])[tid + q * kKs5Threads] = p[q];
     put_digits(0);
     __syncthreads();
-    ks5_v16i acc = {};
-    const int row = wave * 32 + r;
+    ks5_v16i acc[MS];
+#pragma unroll
+    for (int m = 0; m < MS; ++m) acc[m] = ks5_v16i{};
     for (int c = 0; c < kChunks; ++c) {
         const bool more = c + 1 < kChunks;
         {   // next chunk in flight during this one (the last iteration reloads its own: harmless)
@@ -531,32 +543,43 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
             const uint4 *sn = src + (size_t)cn * kKs5ChU4;
 #pragma unroll
             for (int q = 0; q < kKs5Pieces; ++q) p[q] = sn[q * kKs5Threads];
-            u0 = pa[cn * (kKs5Ch / 4)];
-            u1 = pa[cn * (kKs5Ch / 4) + 1];
-            v0 = pa2[cn * (kKs5Ch / 4)];
-            v1 = pa2[cn * (kKs5Ch / 4) + 1];
+#pragma unroll
+            for (int q = 0; q < kU4; ++q) {
+                uu[q] = pa[cn * (kKs5Ch / 4) + q];
+                vv[q] = pa2[cn * (kKs5Ch / 4) + q];
+            }
         }
-        const uint4 xd = *reinterpret_cast<const uint4 *>(&dg[c & 1][hh][row][0]);
-        const uint32_t xw[4] = {xd.x, xd.y, xd.z, xd.w};
+        uint32_t xw[MS][4];
+#pragma unroll
+        for (int m = 0; m < MS; ++m) {
+            const uint4 xd = *reinterpret_cast<const uint4 *>(&dg[c & 1][hh][wave * 32 * MS + 32 * m + r][0]);
+            xw[m][0] = xd.x; xw[m][1] = xd.y; xw[m][2] = xd.z; xw[m][3] = xd.w;
+        }
         const uint4(*cur)[64] = bs[c & 1];
-        // fragments read in groups of kKs5G (all reads of a group issued before its MFMAs)
+        // fragments read in groups of kG i-steps (all reads of a group issued before its MFMAs)
 #pragma unroll
-        for (int g = 0; g < kKs5Ch; g += kKs5G) {
-            uint4 av[kKs5G], bv[kKs5G];
+        for (int g = 0; g < kKs5Ch; g += kG) {
+            uint4 av[MS][kG], bv[kG];
 #pragma unroll
-            for (int q = 0; q < kKs5G; ++q) {
+            for (int q = 0; q < kG; ++q) {
                 const int ii = g + q;
-                const uint32_t xb = xw[ii >> 2] >> (8 * (ii & 3));   // digits a_{4hh..4hh+3}, high first
-                const uint2 d01 = lut[(xb >> 4) & 15u][r], d23 = lut[xb & 15u][r];
-                av[q] = make_uint4(d01.x, d01.y, d23.x, d23.y);
+#pragma unroll
+                for (int m = 0; m < MS; ++m) {
+                    const uint32_t xb = xw[m][ii >> 2] >> (8 * (ii & 3));   // digits a_{4hh..4hh+3}, high first
+                    const uint2 d01 = lut[(xb >> 4) & 15u][r], d23 = lut[xb & 15u][r];
+                    av[m][q] = make_uint4(d01.x, d01.y, d23.x, d23.y);
+                }
                 bv[q] = cur[ii][l];
             }
             __builtin_amdgcn_sched_barrier(0);   // keep the group's reads ahead of its MFMAs
 #pragma unroll
-            for (int q = 0; q < kKs5G; ++q) {
-                const ks5_v4i a = {(int)av[q].x, (int)av[q].y, (int)av[q].z, (int)av[q].w};
+            for (int q = 0; q < kG; ++q) {
                 const ks5_v4i b = {(int)bv[q].x, (int)bv[q].y, (int)bv[q].z, (int)bv[q].w};
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < MS; ++m) {
+                    const ks5_v4i a = {(int)av[m][q].x, (int)av[m][q].y, (int)av[m][q].z, (int)av[m][q].w};
+                    acc[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[m], 0, 0, 0);
+                }
             }
         }
         if (more) {                              // other buffers: every wave finished them a chunk ago
@@ -567,21 +590,24 @@ __global__ __launch_bounds__(kKs5Threads) void k_keyswitch_v5(const uint4 *__res
         __syncthreads();
     }
     // limbs -> Torus32: lane l holds column nb * 8 + (l & 31) / 4, limb l & 3, and ciphertext rows
-    // (reg & 3) + 8 (reg >> 2) + 4 hh of the wave's 32; the quad of lanes 4 q .. 4 q + 3 sums
+    // (reg & 3) + 8 (reg >> 2) + 4 hh of each 32-row slice; the quad of lanes 4 q .. 4 q + 3 sums
     // its limbs shifted into place (wrapping: exact mod 2^32) and its first lane stores
     const int col = nb * 8 + (r >> 2);
     const uint32_t lsh = 8u * (uint32_t)(l & 3);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        uint32_t v = (uint32_t)acc[reg] << lsh;
-        v += (uint32_t)__shfl_xor((int)v, 1, 64);
-        v += (uint32_t)__shfl_xor((int)v, 2, 64);
-        const int ctm = mt * (32 * kKs5Waves) + wave * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
-        if ((l & 3) == 0 && ctm < io.count() && col <= kn) {
-            const KsLane lm = io.lane(ctm);
-            if (SPLIT > 1) atomicAdd(reinterpret_cast<unsigned int *>(col < kn ? lm.ra + col : lm.rb), 0u - v);
-            else if (col < kn) lm.ra[col] = (int32_t)(0u - v);
-            else *lm.rb = (int32_t)(lm.b - v);
+    for (int m = 0; m < MS; ++m) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            uint32_t v = (uint32_t)acc[m][reg] << lsh;
+            v += (uint32_t)__shfl_xor((int)v, 1, 64);
+            v += (uint32_t)__shfl_xor((int)v, 2, 64);
+            const int ctm = mt * kM + wave * 32 * MS + 32 * m + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
+            if ((l & 3) == 0 && ctm < io.count() && col <= kn) {
+                const KsLane lm = io.lane(ctm);
+                if (SPLIT > 1) atomicAdd(reinterpret_cast<unsigned int *>(col < kn ? lm.ra + col : lm.rb), 0u - v);
+                else if (col < kn) lm.ra[col] = (int32_t)(0u - v);
+                else *lm.rb = (int32_t)(lm.b - v);
+            }
         }
     }
 }
@@ -661,20 +687,26 @@ static int ks5_split(int mtiles) {
     while (sp < 8 && mtiles * kKs5Nb * sp < 512) sp *= 2;
     return sp;
 }
+template <class P, int MS>
+static void launch_ks5(const uint4 *w5, int count, const P &io, hipStream_t s) {
+    const int mtiles = (count + 32 * kKs5Waves * MS - 1) / (32 * kKs5Waves * MS);
+    const int split = ks5_split(mtiles);
+    if (split > 1) hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
+    const dim3 grid(mtiles * kKs5Nb * split);
+    switch (split) {
+    case 8: hipLaunchKernelGGL((k_keyswitch_v5<P, 8, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+    case 4: hipLaunchKernelGGL((k_keyswitch_v5<P, 4, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+    case 2: hipLaunchKernelGGL((k_keyswitch_v5<P, 2, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+    default: hipLaunchKernelGGL((k_keyswitch_v5<P, 1, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
+    }
+}
 template <class P>
 static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io, hipStream_t s) {
     if (key.ksk5) {
-        const int mtiles = (count + 32 * kKs5Waves - 1) / (32 * kKs5Waves);
         const uint4 *w5 = reinterpret_cast<const uint4 *>(key.ksk5);
-        const int split = ks5_split(mtiles);
-        if (split > 1) hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
-        const dim3 grid(mtiles * kKs5Nb * split);
-        switch (split) {
-        case 8: hipLaunchKernelGGL((k_keyswitch_v5<P, 8>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
-        case 4: hipLaunchKernelGGL((k_keyswitch_v5<P, 4>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
-        case 2: hipLaunchKernelGGL((k_keyswitch_v5<P, 2>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
-        default: hipLaunchKernelGGL((k_keyswitch_v5<P, 1>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
-        }
+        // one M-slice per wave: two slices sharing each B-fragment read (MS = 2, 157 VGPRs) measured
+        // slower at every batch (B = 1024 0.089 -> 0.128 ms, 4096 0.306 -> 0.399)
+        launch_ks5<P, 1>(w5, count, io, s);
         return;
     }
     if (count <= ks_split_max()) {
