@@ -238,7 +238,30 @@ __device__ __forceinline__ void fft_fwd_AB(Cx (&x)[NP][8], double2 *X, const dou
 template <int NP>
 __device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const Tw4 &tA, const Tw4 &t, int L) {
     pass_fwd<NP>(x, tA.w0, tA.w1, tA.w2a, tA.w2b);
-#ifndef TFHE_AMD_DIAG_NOTRAB
+#if defined(TFHE_AMD_DIAG_PERMFWD)
+    // timing diagnostic (wrong results): the forward A -> B transpose replaced by the cross-lane
+    // work a radix-16 forward would need instead (2 x 32 v_permlane{16,32}_swap on the doubles
+    // + 16 on the digit words), to price that design before building it
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int r = 0; r < 8; r += 2) {
+            unsigned *a = reinterpret_cast<unsigned *>(&x[p][r]);
+            unsigned *b = reinterpret_cast<unsigned *>(&x[p][r + 1]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                auto s16 = __builtin_amdgcn_permlane16_swap(a[k], b[k], false, false);
+                auto s32 = __builtin_amdgcn_permlane32_swap(s16[0], s16[1], false, false);
+                a[k] = s32[0];
+                b[k] = s32[1];
+            }
+            if (r < 4) {
+                auto s = __builtin_amdgcn_permlane32_swap(a[0], b[2], false, false);
+                a[0] = s[0];
+                b[2] = s[1];
+            }
+        }
+#elif !defined(TFHE_AMD_DIAG_NOTRAB) && !defined(TFHE_AMD_DIAG_FWDNOTR)
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         store_A(X, x[p], L);
