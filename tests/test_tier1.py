@@ -38,6 +38,21 @@ def test_tier1_threads_and_aliasing_gpu():
 
 
 @pytest.mark.gpu
+def test_tier1_single_gate_latency():
+    """Sequential single-gate calls through the C API (what an unchanged Cipher.cpp caller sees):
+    chained bootsNAND decrypt right and cost about one B = 1 device step (1.7 ms) plus the
+    synchronous host round trip and the current_variance bookkeeping."""
+    exe = os.path.join(CALLERS, "_bin", "tier1_latency")
+    assert os.access(exe, os.X_OK), "tests/callers/_bin/tier1_latency missing: run __graft_entry__.build()"
+    r = subprocess.run([exe, "20"], capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines and r.returncode == 0, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
+    out = json.loads(lines[-1])
+    print(out)
+    assert out["decrypt_ok"] and out["tier1_ms_per_gate"] < 5.0, out
+
+
+@pytest.mark.gpu
 def test_tier1_current_variance_as_reference(keyset, okey, rng):
     """current_variance after bootsNAND / bootsMUX (Tier-1, through the C ABI): the reference's
     lweKeySwitch restarts it at 0 and adds the variance of every key-switching-key row its
