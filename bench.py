@@ -61,7 +61,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first: the clock and power state settle within ~10 (2: -2 %%)")
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
     ap.add_argument("--extra-batches", default="1,4096", help="per-GPU batch sizes also timed ('none' = none)")
