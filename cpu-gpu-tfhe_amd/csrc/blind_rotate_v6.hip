@@ -92,12 +92,17 @@ __device__ __forceinline__ unsigned int hwreg_xcc_id() {
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
 
-struct __attribute__((aligned(16))) V6Shared {
+struct __attribute__((aligned(16))) V6Ct {   // one ciphertext's LDS
     double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
-    double2 tw[kT7Words];            // per-lane twiddles (compact table, fft_wave.h)
 };
+template <int C>
+struct __attribute__((aligned(16))) V6SharedC {
+    V6Ct ct[C];                      // C ciphertexts per workgroup share ...
+    double2 tw[kT7Words];            // ... the per-lane twiddles (compact table, fft_wave.h)
+};
+using V6Shared = V6SharedC<1>;
 static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave buffer");
 
 struct V6Args {
@@ -142,7 +147,7 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
 template <int WAVES>
-__device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
+__device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
@@ -187,7 +192,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
 #ifdef TFHE_AMD_DIAG_NOTW   // timing diagnostic (wrong results): twiddles from registers, no LDS loads
 #define TW7(fn) diag_tw(L)
 #else
-#define TW7(fn) fn(sh.tw, L)
+#define TW7(fn) fn(shtw, L)
 #endif
     fft_fwd_AB_t<2>(D, X, tA, TW7(tw7_fwdB), L);
     V6_STAMP(1);
@@ -257,7 +262,7 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
         }
 #else
 #pragma unroll
-        for (int r = 0; r < 8; ++r) z[r] = ld(sh.tw + kT7Post + r * 64 + L);
+        for (int r = 0; r < 8; ++r) z[r] = ld(shtw + kT7Post + r * 64 + L);
 #endif
 #ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
@@ -286,10 +291,15 @@ __device__ __forceinline__ void cmux_v6(V6Shared &sh, const V6Args &g, const Tw4
     V6_STAMP(8);
 }
 
-template <int WAVES>
-__device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const RowTerms6 &t, int32_t mu,
-                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot) {
-    const int tid = threadIdx.x;
+// C ciphertexts per workgroup (128 C threads; ciphertext threadIdx.x / 128 uses sh): with C = 2
+// the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
+// exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
+// computes but writes nothing.
+template <int WAVES, int C = 1>
+__device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
+                                           int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
+                                           bool live = true) {
+    const int tid = threadIdx.x & (kV6Threads - 1);
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
 #ifdef TFHE_AMD_V6_STAMPS
@@ -314,7 +324,7 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
         if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
-    for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
+    for (int e = threadIdx.x; e < kT7Words; e += C * kV6Threads) shtw[e] = g.tw[t7_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
@@ -346,10 +356,10 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
-        if (a == 0) continue;            // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES>(sh, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
+        if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
+        cmux_v6<WAVES>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
     }
-    if (g.flags) {   // exactness guard: this wave's largest rounding distance (high word)
+    if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
         if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
         const uint32_t h = wave_max_hi(mx);
         if (L == 0) {
@@ -364,7 +374,8 @@ __device__ __forceinline__ void br_v6_body(V6Shared &sh, const V6Args &g, const 
     // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]; the other
     // wave may still be in its last inverse in either buffer
     __syncthreads();
-    if (w == 0) {
+    if (!live) {
+    } else if (w == 0) {
         uint32_t *E = reinterpret_cast<uint32_t *>(sh.X[0]);
         write_ext(E, acc, L);
         wave_sync();
@@ -398,7 +409,31 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g,
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES>(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
+    br_v6_body<WAVES>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
+}
+
+// two ciphertexts per workgroup (4 waves): the dispatcher spreads a 4-wave workgroup over the
+// CU's 4 SIMDs, where two 2-wave workgroups sharing a CU land on 3 of them (2, 1, 1, 0 waves;
+// scripts/wave_placement.hip), so at B <= 2 CUs this keeps one wave per SIMD
+template <int WAVES>
+__global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Args g, int B, int total, int base,
+                                                                     BrInput in0, BrInput in1, int32_t mu,
+                                                                     int32_t *__restrict__ u_a,
+                                                                     int32_t *__restrict__ u_b) {
+    __shared__ V6SharedC<2> sh;
+    const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    int gct = base + 2 * (int)blockIdx.x + s;
+    const bool live = gct < total;
+    if (!live) gct = total - 1;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+    RowTerms6 t;
+    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+    t.za = nullptr; t.zb = nullptr;
+    br_v6_body<WAVES, 2>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
 template <int WAVES>
@@ -424,7 +459,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Ar
     wire(row.y, t.ya, t.yb);
     wire(row.z, t.za, t.zb);
     const size_t slot = (size_t)r * B + k;
-    br_v6_body<WAVES>(sh, g, t, mu, u_a + slot * kN, u_b + slot, slot);
+    br_v6_body<WAVES>(sh.ct[0], sh.tw, g, t, mu, u_a + slot * kN, u_b + slot, slot);
 }
 
 __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
@@ -437,20 +472,20 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
     uint32_t ac[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) ac[r] = (uint32_t)accg[L + 64 * r];
-    for (int i = tid; i < iters; i += kV6Threads) sh.bara[i] = (short)(bara[(size_t)blockIdx.x * iters + i] & (k2N - 1));
+    for (int i = tid; i < iters; i += kV6Threads) sh.ct[0].bara[i] = (short)(bara[(size_t)blockIdx.x * iters + i] & (k2N - 1));
     for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     int own = w;
     for (int i = 0; i < iters; ++i) {
-        const int a = sh.bara[i];
+        const int a = sh.ct[0].bara[i];
         if (a == 0) continue;
 #ifdef TFHE_AMD_V6_STAMPS
         V6Stamps stamps;
 #endif
         double mx = 0.0;
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
-        cmux_v6<2>(sh, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<2>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -553,6 +588,19 @@ static long v6_chunk(const DeviceKey &key) {
     const long c = env ? atol(env) : 4L * v6_cus(key);
     return c > 0 ? c : (1L << 40);
 }
+// Two ciphertexts per workgroup (k_blind_rotate_v6p) for a launch of n ciphertexts when
+// CUs < n <= 2 CUs: then at most one 4-wave workgroup per CU, one wave per SIMD, where 2-wave
+// workgroups would pair up on some CUs over 3 SIMDs (B = 512: 2.36 -> 2.30 ms).  At n <= CUs
+// one 2-wave workgroup per CU is faster (B = 256: 1.74 vs 2.29 ms: 2 waves on a CU run each step
+// faster than 4 — LDS and the key path are shared per CU), and above 2 CUs the 2-wave
+// workgroups fill every SIMD (B = 768: 2.62 vs 3.18 ms, 1024: 3.12 vs 3.26).
+// TFHE_AMD_V6_PAIR=0/1 forces it off/on (experiments).
+static bool v6_pair(const DeviceKey &key, long n) {
+    static const char *env = getenv("TFHE_AMD_V6_PAIR");
+    if (env) return atoi(env) != 0;
+    const long cus = v6_cus(key);
+    return n > cus && n <= 2 * cus;
+}
 static int v6_prio_policy(const DeviceKey &key, long wgs) {
     static const char *env = getenv("TFHE_AMD_PRIO");
     if (env) return atoi(env);
@@ -580,8 +628,14 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                           v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
+        if (v6_pair(key, n)) {
+            const long wgs = (n + 1) / 2;
+            hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                               v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+        } else {
+            hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                               v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
+        }
     }
     return hipGetLastError();
 }

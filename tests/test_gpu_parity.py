@@ -156,6 +156,33 @@ def test_chunk_boundaries_bit_exact(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
+def test_paired_workgroups_bit_exact(ctx, okey, keyset, rng):
+    """Launches of CUs < n <= 2 CUs ciphertexts (256 CUs) run two ciphertexts per workgroup
+    (k_blind_rotate_v6p): an odd count (a padding ciphertext that writes nothing), MUX halves
+    meeting inside one workgroup, and a_i = 0 steps, which the paired kernel runs as identity
+    CMuxes instead of skipping — every output against the oracle."""
+    B = 301
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    r_a, r_b = ctx.gate_host("AND", a_a, a_b, b_a, b_b)
+    o_a, o_b = okey.gate_batch("AND", a_a, a_b, b_a, b_b)
+    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
+    B = 199                                   # MUX: 398 rotations; rotations 198 | 199 share a workgroup
+    s, x, y = (rng.integers(0, 2, B) for _ in range(3))
+    (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
+    r_a, r_b = ctx.gate_host("MUX", sa, sb, xa, xb, ya, yb)
+    o_a, o_b = okey.gate_batch("MUX", sa, sb, xa, xb, ya, yb)
+    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
+    B = 300
+    x_a = rng.integers(-2**31, 2**31, (B, n), dtype=np.int64).astype(np.int32)
+    x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    x_a[::3, :40] = 0                         # runs of bara = 0 in every third ciphertext
+    x_a[1::7, 100:140] = np.int32(-(2**20))   # bara = 0 through the wrap
+    u_a, u_b = ctx.woks_host(T.MU, x_a, x_b)
+    o_a, o_b = okey.woks_batch(T.MU, x_a, x_b)
+    assert np.array_equal(u_a, o_a) and np.array_equal(u_b, o_b)
+
+
 def test_device_api_rejects_bad_tensors(ctx):
     """Shapes, dtypes, missing MUX inputs and tensors on another GPU are refused on the host,
     before any launch."""
