@@ -205,49 +205,66 @@ __device__ __forceinline__ bool guard_skip(const V4Guard &gd, size_t slot) {
     return false;
 }
 
-// gate batch: ciphertext gct of half h = gct / B reads in_h at index gct mod B
-__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4(V4Args g, int B, BrInput in0, BrInput in1,
-                                                                int32_t mu, int32_t *__restrict__ u_a,
+// gate batch: ciphertext gct of half h = gct / B reads in_h at index gct mod B.  Grid-stride
+// over the total ciphertexts: one per workgroup normally; in guard mode a small grid scans the
+// flags (almost always all clear) instead of dispatching one workgroup per ciphertext.
+// MINW: waves per SIMD the register budget is cut for — 2 for the exact throughput kernel
+// (TFHE_AMD_BR=4: 256 VGPRs, 27 spilled), 1 for the guard launch (284 VGPRs, no scratch: a
+// kernel with a private segment costs ~12 us more per dispatch even when every workgroup exits
+// at once)
+template <int MINW>
+__global__ __launch_bounds__(kV4Threads, MINW) void k_blind_rotate_v4(V4Args g, int B, int total, BrInput in0,
+                                                                BrInput in1, int32_t mu,
+                                                                int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b, V4Guard gd) {
     __shared__ V4Shared sh;
-    const int gct = blockIdx.x;
-    if (guard_skip(gd, (size_t)gct)) return;
-    const int half = gct >= B;
-    const int idx = half ? gct - B : gct;
-    const BrInput &in = half ? in1 : in0;
-    RowTerms t;
-    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
-    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
-    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
-    t.za = nullptr; t.zb = nullptr;
-    br_v4_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+    bool used = false;
+    for (int gct = blockIdx.x; gct < total; gct += gridDim.x) {
+        if (guard_skip(gd, (size_t)gct)) continue;
+        if (used) __syncthreads();   // the previous ciphertext's extraction has read the LDS
+        used = true;
+        const int half = gct >= B;
+        const int idx = half ? gct - B : gct;
+        const BrInput &in = half ? in1 : in0;
+        RowTerms t;
+        t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+        t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+        t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+        t.za = nullptr; t.zb = nullptr;
+        br_v4_body(sh, g, t, mu, u_a + (size_t)gct * kN, u_b + gct);
+    }
 }
 
-// circuit level: blockIdx.x = instance k < B, blockIdx.y = row r; wires are [W][B] ciphertexts,
-// the extracted sample of (r, k) goes to u slot r B + k
-__global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_rows(V4Args g, int B, const CircRow *__restrict__ rows,
+// circuit level: flat slot r B + k (row r, instance k < B), grid-stride as the gate kernel;
+// wires are [W][B] ciphertexts, the extracted sample of (r, k) goes to u slot r B + k
+template <int MINW>
+__global__ __launch_bounds__(kV4Threads, MINW) void k_blind_rotate_v4_rows(V4Args g, int B, long total,
+                                                                     const CircRow *__restrict__ rows,
                                                                      const int32_t *__restrict__ wa,
                                                                      const int32_t *__restrict__ wb, int32_t mu,
                                                                      int32_t *__restrict__ u_a,
-                                                                     int32_t *__restrict__ u_b, int row0,
-                                                                     V4Guard gd) {
+                                                                     int32_t *__restrict__ u_b, V4Guard gd) {
     __shared__ V4Shared sh;
-    const int k = blockIdx.x, r = row0 + (int)blockIdx.y;
-    if (guard_skip(gd, (size_t)r * B + k)) return;
-    const CircRow row = rows[r];
-    auto wire = [&](int w, const int32_t *&pa, const int32_t *&pb) {
-        if (w < 0) { pa = nullptr; pb = nullptr; return; }
-        const size_t slot = (size_t)w * B + k;
-        pa = wa + slot * kn;
-        pb = wb + slot;
-    };
-    RowTerms t;
-    t.c = row.c; t.sa = row.sa; t.sb = row.sb; t.sc = row.sc;
-    wire(row.x, t.xa, t.xb);
-    wire(row.y, t.ya, t.yb);
-    wire(row.z, t.za, t.zb);
-    const size_t slot = (size_t)r * B + k;
-    br_v4_body(sh, g, t, mu, u_a + slot * kN, u_b + slot);
+    bool used = false;
+    for (long slot = blockIdx.x; slot < total; slot += gridDim.x) {
+        if (guard_skip(gd, (size_t)slot)) continue;
+        if (used) __syncthreads();
+        used = true;
+        const int r = (int)(slot / B), k = (int)(slot - (long)r * B);
+        const CircRow row = rows[r];
+        auto wire = [&](int w, const int32_t *&pa, const int32_t *&pb) {
+            if (w < 0) { pa = nullptr; pb = nullptr; return; }
+            const size_t ws = (size_t)w * B + k;
+            pa = wa + ws * kn;
+            pb = wb + ws;
+        };
+        RowTerms t;
+        t.c = row.c; t.sa = row.sa; t.sb = row.sb; t.sc = row.sc;
+        wire(row.x, t.xa, t.xb);
+        wire(row.y, t.ya, t.yb);
+        wire(row.z, t.za, t.zb);
+        br_v4_body(sh, g, t, mu, u_a + (size_t)slot * kN, u_b + slot);
+    }
 }
 
 __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_debug(V4Args g, int iters, int32_t *__restrict__ acc,
@@ -319,6 +336,7 @@ static V4Args v4_args(const DeviceKey &key) {
     return g;
 }
 
+constexpr int kGuardGrid = 256;
 static V4Guard v4_guard(const Guard *guard) {
     V4Guard gd{nullptr, 0u, nullptr};
     if (guard && guard->flags) gd = V4Guard{guard->flags, guard_threshold_hi(), guard->stats};
@@ -330,8 +348,16 @@ hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const
     if (B <= 0) return hipSuccess;
     if (!key.bk_v2) return hipErrorInvalidValue;
     const BrInput in1 = halves > 1 ? in[1] : in[0];
-    hipLaunchKernelGGL(k_blind_rotate_v4, dim3(B * halves), dim3(kV4Threads), 0, s, v4_args(key), B, in[0], in1, mu,
-                       u_a, u_b, v4_guard(guard));
+    const V4Guard gd = v4_guard(guard);
+    const int total = B * halves;
+    // guard mode: 256 workgroups scan the flags (B = 1024: 15 -> ~4 us per launch)
+    const int grid = gd.flags && total > kGuardGrid ? kGuardGrid : total;
+    if (gd.flags)
+        hipLaunchKernelGGL(k_blind_rotate_v4<1>, dim3(grid), dim3(kV4Threads), 0, s, v4_args(key), B, total, in[0],
+                           in1, mu, u_a, u_b, gd);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_v4<2>, dim3(grid), dim3(kV4Threads), 0, s, v4_args(key), B, total, in[0],
+                           in1, mu, u_a, u_b, gd);
     return hipGetLastError();
 }
 
@@ -340,11 +366,15 @@ hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, c
                                        const Guard *guard) {
     if (B <= 0 || nrows <= 0) return hipSuccess;
     if (!key.bk_v2) return hipErrorInvalidValue;
-    for (int r0 = 0; r0 < nrows; r0 += 65535) {   // grid y is limited to 65535 rows per launch
-        const int n = nrows - r0 < 65535 ? nrows - r0 : 65535;
-        hipLaunchKernelGGL(k_blind_rotate_v4_rows, dim3(B, n), dim3(kV4Threads), 0, s, v4_args(key), B, rows, wa, wb,
-                           mu, u_a, u_b, r0, v4_guard(guard));
-    }
+    const V4Guard gd = v4_guard(guard);
+    const long total = (long)B * nrows;
+    const long grid = gd.flags && total > kGuardGrid ? kGuardGrid : total < 0x7fffffffL ? total : 0x7fffffffL;
+    if (gd.flags)
+        hipLaunchKernelGGL(k_blind_rotate_v4_rows<1>, dim3((unsigned)grid), dim3(kV4Threads), 0, s, v4_args(key), B,
+                           total, rows, wa, wb, mu, u_a, u_b, gd);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_v4_rows<2>, dim3((unsigned)grid), dim3(kV4Threads), 0, s, v4_args(key), B,
+                           total, rows, wa, wb, mu, u_a, u_b, gd);
     return hipGetLastError();
 }
 

@@ -103,6 +103,25 @@ def test_guard_forced_fallback_bit_exact(ctx, okey, keyset, rng):
 
 
 @pytest.mark.gpu
+def test_guard_forced_fallback_grid_stride(ctx, okey, keyset, rng):
+    """More flagged ciphertexts than the guard launch has workgroups (256): each workgroup
+    recomputes several in turn; every output still equals the oracle's."""
+    B = 300
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    ctx.guard_stats(reset=True)
+    try:
+        T.set_guard_threshold(0.0)
+        r = ctx.gate_host("OR", a_a, a_b, b_a, b_b)
+        _, redo = ctx.guard_stats(reset=True)
+    finally:
+        T.set_guard_threshold(0.25)
+    assert redo == B
+    want = okey.gate_batch("OR", a_a, a_b, b_a, b_b)
+    assert np.array_equal(r[0], want[0]) and np.array_equal(r[1], want[1])
+
+
+@pytest.mark.gpu
 def test_guard_catches_worst_case_key(keyset, rng):
     """The constructed key: the fp64 kernel's rounding distance reaches the threshold, the
     exact kernel recomputes those ciphertexts, and the woKS outputs equal the exact oracle's."""
