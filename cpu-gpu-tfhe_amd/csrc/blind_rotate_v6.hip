@@ -146,7 +146,7 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
-template <int WAVES>
+template <int WAVES, bool RREG>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
@@ -162,29 +162,62 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 #define KEYC(c) (c)
 #endif
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
-#ifndef TFHE_AMD_DIAG_NOEXT   // timing diagnostic (wrong results): no accumulator-extension stores
-    write_ext(E, acc, L);
-#endif
-    wave_sync();
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
     Cx D[2][8];
+    auto digits = [&](int r, uint32_t rot) {
+        const uint32_t diff = rot - acc[r];
+        const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
+        const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
+        if (r < 8) {
+            D[0][r].re = (double)hi;
+            D[1][r].re = (double)lo;
+        } else {
+            D[0][r - 8].im = (double)hi;
+            D[1][r - 8].im = (double)lo;
+        }
+    };
+    if constexpr (RREG) {
+        // X^a ACC_w without the LDS extension: coefficient j = L + 64 r needs (j - a) mod 2N; with
+        // a = 64 q + s, lane L takes lane (L - s) mod 64's register r - q (r - q - 1 for L < s)
+        // of the negacyclic ring of 32 registers (16 held, the other 16 their negatives): one
+        // ds_bpermute per register, then a rotation by the wave-uniform q in 5 binary stages.
+        // Used for launches of more than one workgroup per CU (B = 512 / 1024 / 4096: -1.0 /
+        // -0.8 / -0.7 %); the LDS extension stays for the latency case (B = 1: 1.68 vs 1.70 ms).
+        (void)E;
+        const int aa = __builtin_amdgcn_readfirstlane(a) & (k2N - 1);
+        const int s = aa & 63, q = aa >> 6;
+        const int src = ((L - s) & 63) << 2;
+        uint32_t V[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int base = (L + 256 * q - a) & (k2N - 1);
+        for (int r = 0; r < 16; ++r) V[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)acc[r]);
+        if (q & 16) {
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int r = 4 * q + rr;
-            const uint32_t diff = E[base + 64 * rr] - acc[r];
-            const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
-            const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
-            if (r < 8) {
-                D[0][r].re = (double)hi;
-                D[1][r].re = (double)lo;
-            } else {
-                D[0][r - 8].im = (double)hi;
-                D[1][r - 8].im = (double)lo;
+            for (int r = 0; r < 16; ++r) V[r] = 0u - V[r];
+        }
+#pragma unroll
+        for (int K = 8; K >= 1; K >>= 1) {
+            if (q & K) {
+                uint32_t t[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t[r] = r >= K ? V[r - K] : 0u - V[r + 16 - K];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) V[r] = t[r];
             }
+        }
+        const bool lo = L < s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) digits(r, lo ? (r ? V[r - 1] : 0u - V[15]) : V[r]);
+    } else {
+#ifndef TFHE_AMD_DIAG_NOEXT   // timing diagnostic (wrong results): no accumulator-extension stores
+        write_ext(E, acc, L);
+#endif
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int base = (L + 256 * q - a) & (k2N - 1);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) digits(4 * q + rr, E[base + 64 * rr]);
         }
     }
     wave_sync();
@@ -295,7 +328,7 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 // the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
 // exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
 // computes but writes nothing.
-template <int WAVES, int C = 1>
+template <int WAVES, bool RREG, int C = 1>
 __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
                                            bool live = true) {
@@ -357,7 +390,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
         if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
@@ -395,7 +428,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
 #endif
 }
 
-template <int WAVES>
+template <int WAVES, bool RREG>
 __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g, int B, int base, BrInput in0,
                                                                 BrInput in1, int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
@@ -409,7 +442,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g,
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
+    br_v6_body<WAVES, RREG>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
 }
 
 // two ciphertexts per workgroup (4 waves): the dispatcher spreads a 4-wave workgroup over the
@@ -433,10 +466,10 @@ __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Ar
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES, 2>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
+    br_v6_body<WAVES, true, 2>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
-template <int WAVES>
+template <int WAVES, bool RREG>
 __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, long base,
                                                                      const CircRow *__restrict__ rows,
                                                                      const int32_t *__restrict__ wa,
@@ -459,9 +492,10 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Ar
     wire(row.y, t.ya, t.yb);
     wire(row.z, t.za, t.zb);
     const size_t slot = (size_t)r * B + k;
-    br_v6_body<WAVES>(sh.ct[0], sh.tw, g, t, mu, u_a + slot * kN, u_b + slot, slot);
+    br_v6_body<WAVES, RREG>(sh.ct[0], sh.tw, g, t, mu, u_a + slot * kN, u_b + slot, slot);
 }
 
+template <bool RREG>
 __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args g, int iters, int32_t *__restrict__ acc,
                                                                       const int32_t *__restrict__ bara) {
     __shared__ V6Shared sh;
@@ -485,7 +519,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #endif
         double mx = 0.0;
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
-        cmux_v6<2>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<2, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -601,6 +635,13 @@ static bool v6_pair(const DeviceKey &key, long n) {
     const long cus = v6_cus(key);
     return n > cus && n <= 2 * cus;
 }
+// the register / ds_bpermute rotation (cmux_v6 RREG) for launches of more than one workgroup
+// per CU; TFHE_AMD_V6_RREG=0/1 forces it off/on (experiments, tests)
+static bool v6_rreg(const DeviceKey &key, long n) {
+    static const char *env = getenv("TFHE_AMD_V6_RREG");
+    if (env) return atoi(env) != 0;
+    return n > v6_cus(key);
+}
 static int v6_prio_policy(const DeviceKey &key, long wgs) {
     static const char *env = getenv("TFHE_AMD_PRIO");
     if (env) return atoi(env);
@@ -633,8 +674,12 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
             hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
                                v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
         } else {
-            hipLaunchKernelGGL(k_blind_rotate_v6<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                               v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
+            if (v6_rreg(key, n))
+                hipLaunchKernelGGL((k_blind_rotate_v6<kV6Waves, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                                   v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
+            else
+                hipLaunchKernelGGL((k_blind_rotate_v6<kV6Waves, false>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                                   v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
         }
     }
     return hipGetLastError();
@@ -649,8 +694,12 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
         if (n > 0x7fffffffL) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_blind_rotate_v6_rows<kV6Waves>, dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                           v6_args(key, n, guard), B, base, rows, wa, wb, mu, u_a, u_b);
+        if (v6_rreg(key, n))
+            hipLaunchKernelGGL((k_blind_rotate_v6_rows<kV6Waves, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                               v6_args(key, n, guard), B, base, rows, wa, wb, mu, u_a, u_b);
+        else
+            hipLaunchKernelGGL((k_blind_rotate_v6_rows<kV6Waves, false>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                               v6_args(key, n, guard), B, base, rows, wa, wb, mu, u_a, u_b);
     }
     return hipGetLastError();
 }
@@ -659,7 +708,12 @@ hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, 
                                         hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (iters < 0 || iters > kn || !key.bk_fft) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_v6_debug, dim3(B), dim3(kV6Threads), 0, s, v6_args(key, 0), iters, acc, bara);
+    if (v6_rreg(key, B))
+        hipLaunchKernelGGL(k_blind_rotate_v6_debug<true>, dim3(B), dim3(kV6Threads), 0, s, v6_args(key, 0), iters, acc,
+                           bara);
+    else
+        hipLaunchKernelGGL(k_blind_rotate_v6_debug<false>, dim3(B), dim3(kV6Threads), 0, s, v6_args(key, 0), iters,
+                           acc, bara);
     return hipGetLastError();
 }
 

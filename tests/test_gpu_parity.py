@@ -346,6 +346,46 @@ print("ks-v4 ok", c.key_bytes())
     assert "ks-v4 ok" in r.stdout
 
 
+def test_register_rotation_subprocess():
+    """TFHE_AMD_V6_RREG=1 (read once per process) forces the register / ds_bpermute rotation of
+    cmux_v6 — the default only above one workgroup per CU — onto small launches: the CMux steps
+    at the rotation edges (a = 0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048) and woKS with
+    bara = 0 runs still equal the oracle."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [%r, %r]
+import tfhe_amd as T, oracle_ctypes as O
+K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); o = O.OracleKey(K.bk, K.ksk)
+rng = np.random.default_rng(5)
+B, iters = 4, 10
+acc0 = rng.integers(-2**31, 2**31, (B, 2, 1024), dtype=np.int64).astype(np.int32)
+bara = rng.integers(0, 2049, (B, iters), dtype=np.int64).astype(np.int32)
+bara[0] = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048]
+bara[1] = [127, 128, 129, 960, 1087, 1088, 1984, 2000, 31, 32]
+d_acc = torch.from_numpy(acc0.copy()).cuda()
+c.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), iters); c.sync()
+got = d_acc.cpu().numpy()
+for b in range(B):
+    want = acc0[b].copy()
+    for i in range(iters):
+        if bara[b, i] != 0:
+            want = o.mux_rotate(want, i, int(bara[b, i]))
+    assert np.array_equal(got[b], want), b
+x_a = rng.integers(-2**31, 2**31, (8, 500), dtype=np.int64).astype(np.int32)
+x_b = rng.integers(-2**31, 2**31, 8, dtype=np.int64).astype(np.int32)
+x_a[1, :50] = 0
+u = c.woks_host(T.MU, x_a, x_b); w = o.woks_batch(T.MU, x_a, x_b)
+assert np.array_equal(u[0], w[0]) and np.array_equal(u[1], w[1])
+print("rreg ok")
+""" % (os.path.join(REPO, "cpu-gpu-tfhe_amd"), os.path.join(REPO, "tests"))
+    env = dict(os.environ, TFHE_AMD_V6_RREG="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "rreg ok" in r.stdout
+
+
 def test_fp64_ceiling_measurement():
     """tfhe_amd_fp64_ceiling (bench.py's roofline.sustained): a plausible fp64 rate and clock, and
     the caller's current device left as it was."""
