@@ -24,8 +24,9 @@
 //    integers the exact NTT kernels produce; the mod-2^32 reduction is 3 exact fp64 operations.
 //  * each wave has ONE 9 KB LDS buffer: per step it holds the periodic negacyclic extension
 //    E[k] = +-acc[k mod N] (k < 2240: the rotation X^a reads E[(j - a) mod 2N] with one base per
-//    quarter of the lane's coefficients), then the FFT transposes, then the partial sum handed
-//    to the other wave; the per-lane twiddles are read from a 17 KB LDS copy (36.5 KB per
+//    quarter of the lane's coefficients; launches above one workgroup per CU rotate in registers
+//    with ds_bpermute instead, cmux_v6 RREG), then the FFT transposes, then the partial sum
+//    handed to the other wave; the per-lane twiddles are read from a 17 KB LDS copy (36.5 KB per
 //    ciphertext, 4 workgroups per CU), so the key is the only global load in the loop.
 //  * issue priority is steered per launch (set_prio_level): a rotation phased by the workgroup's
 //    rank on its CU for the one-round launches a batch is split into (by step if the split is
