@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B of library variants in one GPU session: scripts/ab_bench.sh name1 name2 ... ("base" = lib/)
-# (AB_BATCH, AB_REPS).  One summary line per run in gpurun_out/ab_summary.txt.
+# (AB_BATCH, AB_REPS, AB_STEPS, AB_WARMUP).  One summary line per run in gpurun_out/ab_summary.txt.
 set -u
 mkdir -p gpurun_out
 for rep in $(seq 1 ${AB_REPS:-1}); do
@@ -16,7 +16,7 @@ for n in "$@"; do
     *) lib=cpu-gpu-tfhe_amd/variants/$n/libtfhe_amd.so ;;
   esac
   log=gpurun_out/ab_${n}_${AB_BATCH:-1024}_$rep.log
-  TFHE_AMD_GUARD=$guard TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup 1 --batch ${AB_BATCH:-1024} --no-cpu-baseline --no-clock --no-ceiling --extra-batches '' --strong-batch 0 > $log 2>&1
+  TFHE_AMD_GUARD=$guard TFHE_AMD_BR=$br TFHE_AMD_LIB=$lib timeout -k 10 200 python bench.py --steps ${AB_STEPS:-5} --warmup ${AB_WARMUP:-1} --batch ${AB_BATCH:-1024} --no-cpu-baseline --no-clock --no-ceiling --extra-batches '' --strong-batch 0 > $log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; tail -5 $log; exit $rc; }
   python3 -c "
 import json,sys
