@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out
 for ps in $2; do
   p=${ps%%:*}; sft=${ps#*:}
-  TFHE_AMD_PRIO=$p TFHE_AMD_PRIO_S=$sft timeout -k 10 120 python bench.py --steps 10 --warmup 2 --batch $1 --no-cpu-baseline --no-clock --no-ceiling --extra-batches none --strong-batch 0 > gpurun_out/ps_${1}_${p}_${sft}.json 2>&1 || exit 3
+  TFHE_AMD_PRIO=$p TFHE_AMD_PRIO_S=$sft timeout -k 10 120 python bench.py --steps 10 --warmup ${PS_WARMUP:-2} --batch $1 --no-cpu-baseline --no-clock --no-ceiling --extra-batches none --strong-batch 0 > gpurun_out/ps_${1}_${p}_${sft}.json 2>&1 || exit 3
   python3 -c "
 import json
 d=[json.loads(l) for l in open('gpurun_out/ps_${1}_${p}_${sft}.json') if l.startswith('{')][-1]
