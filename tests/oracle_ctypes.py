@@ -95,7 +95,10 @@ class OracleKey:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_key_free(self.h)
+            try:
+                lib().orc_key_free(self.h)
+            except TypeError:   # interpreter shutdown: module globals already cleared
+                pass
             self.h = None
 
     # ---- single-sample ops
