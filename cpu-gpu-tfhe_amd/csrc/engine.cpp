@@ -682,28 +682,27 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
         return rc;
     }
     const size_t A = (size_t)B * kn;
-    // staging layout: [ca_a | cb_a | cc_a | res_a] then [ca_b | cb_b | cc_b | res_b]
+    // staging layout: the inputs contiguous, [ca_a | cb_a | (cc_a) | ca_b | cb_b | (cc_b)], and
+    // the results [res_a | res_b] at 3 (A + B): one copy in and one copy out per call (a
+    // single-gate Tier-1 call is latency-bound; each small copy is a few microseconds)
     int32_t *h = c->h_io;
     int32_t *d = c->io;
     const int nin = mux ? 3 : 2;
-    memcpy(h, ca_a, A * 4);
-    memcpy(h + A, cb_a, A * 4);
-    if (mux) memcpy(h + 2 * A, cc_a, A * 4);
-    int32_t *hb = h + 4 * A;
-    memcpy(hb, ca_b, B * 4);
-    memcpy(hb + B, cb_b, B * 4);
-    if (mux) memcpy(hb + 2 * B, cc_b, B * 4);
-    HIPCHK(hipMemcpyAsync(d, h, nin * A * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d + 4 * A, hb, (size_t)nin * B * 4, hipMemcpyHostToDevice, c->stream));
-    int32_t *db = d + 4 * A;
-    rc = tfhe_amd_gate_batch_dev(c, gate, B, d + 3 * A, db + 3 * B, d, db, d + A, db + B,
+    const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
+    int32_t *hb = h + nin * A, *db = d + nin * A;
+    for (int k = 0; k < nin; ++k) {
+        memcpy(h + k * A, in_a[k], A * 4);
+        memcpy(hb + (size_t)k * B, in_b[k], (size_t)B * 4);
+    }
+    HIPCHK(hipMemcpyAsync(d, h, (size_t)nin * (A + B) * 4, hipMemcpyHostToDevice, c->stream));
+    int32_t *hr = h + 3 * (A + B), *dr = d + 3 * (A + B);
+    rc = tfhe_amd_gate_batch_dev(c, gate, B, dr, dr + A, d, db, d + A, db + B,
                                  mux ? d + 2 * A : nullptr, mux ? db + 2 * B : nullptr, c->stream);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h + 3 * A, d + 3 * A, A * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(hb + 3 * B, db + 3 * B, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(hr, dr, (A + B) * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    memcpy(res_a, h + 3 * A, A * 4);
-    memcpy(res_b, hb + 3 * B, (size_t)B * 4);
+    memcpy(res_a, hr, A * 4);
+    memcpy(res_b, hr + A, (size_t)B * 4);
     return TFHE_AMD_OK;
 }
 
