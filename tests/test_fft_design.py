@@ -71,3 +71,30 @@ def test_p3_distance_to_truncating_fft(rng):
     print(f"P3: truncating-FFT mode differs from the exact product on {frac:.1%} of coefficients "
           f"(max |delta| = {int(delta.max())})")
     assert delta.max() <= 1 and 0.3 < frac < 0.7
+
+
+def _rotate_rreg(acc, a):
+    """numpy restatement of rotate_v6<RREG = true> (blind_rotate_v6.hip): lane L, register r holds
+    coefficient L + 64 r; ds_bpermute from lane (L - s) mod 64, then the uniform register rotation
+    by q in the negacyclic ring of 32 registers, then lanes L < s take one register further."""
+    aa = a & 2047
+    s, q = aa & 63, aa >> 6
+    reg = acc.reshape(16, 64).astype(np.uint32)          # [r][L]
+    V = reg[:, (np.arange(64) - s) % 64]                 # bpermute: V[r][L] = reg[r][(L - s) mod 64]
+    ring = np.concatenate([V, (0 - V.astype(np.int64)).astype(np.uint32)])   # 32 registers
+    Vq = ring[(np.arange(16) - q) % 32]                  # V[r] = ring[r - q]
+    prev = np.concatenate([(0 - Vq[15:16].astype(np.int64)).astype(np.uint32), Vq[:15]])   # V[r - 1]
+    lo = np.arange(64) < s
+    out = np.where(lo[None, :], prev, Vq)
+    return out.reshape(-1)                               # index r * 64 + L = coefficient L + 64 r
+
+
+def test_register_rotation_equals_negacyclic_rotation(rng):
+    """The register rotation gives X^a ACC (negacyclic, mod 2^32) for every a the kernel can see,
+    including 0, multiples of 64 and the wrap through 1024 and 2048."""
+    acc = rng.integers(0, 2**32, 1024, dtype=np.uint64).astype(np.uint32)
+    ext = np.concatenate([acc, (0 - acc.astype(np.int64)).astype(np.uint32)])    # E[k], k < 2N
+    for a in list(range(0, 130)) + [511, 512, 513, 960, 1023, 1024, 1025, 1087, 1088, 1984, 2047, 2048] + \
+            list(rng.integers(0, 2049, 64)):
+        want = ext[(np.arange(1024) - a) % 2048]        # (X^a ACC)[j] = E[(j - a) mod 2N]
+        assert np.array_equal(_rotate_rreg(acc, int(a)), want), a
