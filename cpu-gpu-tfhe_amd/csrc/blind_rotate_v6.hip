@@ -26,7 +26,7 @@
 //    E[k] = +-acc[k mod N] (k < 2240: the rotation X^a reads E[(j - a) mod 2N] with one base per
 //    quarter of the lane's coefficients; launches above one workgroup per CU rotate in registers
 //    with ds_bpermute instead, cmux_v6 RREG), then the FFT transposes, then the partial sum
-//    handed to the other wave; the per-lane twiddles are read from a 17 KB LDS copy (36.5 KB per
+//    handed to the other wave; the per-lane twiddles are read from a 10 KB LDS copy (29.7 KB per
 //    ciphertext, 4 workgroups per CU), so the key is the only global load in the loop.
 //  * issue priority is steered per launch (set_prio_level): a rotation phased by the workgroup's
 //    rank on its CU for the one-round launches a batch is split into (by step if the split is
@@ -101,7 +101,7 @@ struct __attribute__((aligned(16))) V6Ct {   // one ciphertext's LDS
 template <int C>
 struct __attribute__((aligned(16))) V6SharedC {
     V6Ct ct[C];                      // C ciphertexts per workgroup share ...
-    double2 tw[kT7Words];            // ... the per-lane twiddles (compact table, fft_wave.h)
+    double2 tw[kT8Words];            // ... the per-lane twiddles (compact table, fft_wave.h)
 };
 using V6Shared = V6SharedC<1>;
 static_assert(kExt6 * 4 <= kXSlots * 16, "accumulator extension fits the wave buffer");
@@ -287,16 +287,16 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     SCHED_FENCE();
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
+        // post-twist zeta^-n, n = L + 64 r = zeta^-L (lane) x e^{-2 pi i r / 32} (register): the
+        // lane factor scales the pass's inputs — the u inputs of its first butterflies here, the v
+        // inputs through its first twiddle, stored as a zeta^-L — and the register factor its
+        // outputs, from constants: 11 complex products and one twiddle load instead of 8 and 8
+        // (B = 1024: the 8 post-twist loads alone cost 1.3 %)
         const Tw4 tI = TW7(tw7_invA);
-        Cx z[8];                                 // post-twist zeta^-n, n = L + 64 r
 #ifdef TFHE_AMD_DIAG_NOTW
-        {
-            const Tw4 d = diag_tw(L);
-            z[0] = d.w0; z[1] = d.w1; z[2] = d.w2a; z[3] = d.w2b; z[4] = d.w1; z[5] = d.w0; z[6] = d.w2b; z[7] = d.w2a;
-        }
+        const Cx sg = diag_tw(L).w0;
 #else
-#pragma unroll
-        for (int r = 0; r < 8; ++r) z[r] = ld(shtw + kT7Post + r * 64 + L);
+        const Cx sg = ld(shtw + kT8Sig + L);
 #endif
 #ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
@@ -305,13 +305,20 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         load_A(X, Y, L);
         SCHED_FENCE();
 #endif
-        pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const double re = fma_(Y[r].re, z[r].re, -(Y[r].im * z[r].im));
-            const double im = fma_(Y[r].re, z[r].im, Y[r].im * z[r].re);
-            Y[r] = Cx{re, im};
-        }
+        for (int r = 0; r < 8; r += 2) Y[r] = cmul(Y[r], sg);
+        pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
+        constexpr double kOm[8][2] = {
+            {1.0, 0.0},
+            {0.98078528040323044913, -0.19509032201612826785},
+            {0.92387953251128675613, -0.38268343236508977173},
+            {0.83146961230254523708, -0.55557023301960222474},
+            {0.70710678118654752440, -0.70710678118654752440},
+            {0.55557023301960222474, -0.83146961230254523708},
+            {0.38268343236508977173, -0.92387953251128675613},
+            {0.19509032201612826785, -0.98078528040323044913}};
+#pragma unroll
+        for (int r = 1; r < 8; ++r) Y[r] = cmul(Y[r], Cx{kOm[r][0], kOm[r][1]});
     }
     V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im); mx tracks the
@@ -358,7 +365,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
         if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
-    for (int e = threadIdx.x; e < kT7Words; e += C * kV6Threads) shtw[e] = g.tw[t7_src(e)];
+    for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[t8_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
@@ -508,7 +515,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #pragma unroll
     for (int r = 0; r < 16; ++r) ac[r] = (uint32_t)accg[L + 64 * r];
     for (int i = tid; i < iters; i += kV6Threads) sh.ct[0].bara[i] = (short)(bara[(size_t)blockIdx.x * iters + i] & (k2N - 1));
-    for (int e = tid; e < kT7Words; e += kV6Threads) sh.tw[e] = g.tw[t7_src(e)];
+    for (int e = tid; e < kT8Words; e += kV6Threads) sh.tw[e] = g.tw[t8_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
     int own = w;
@@ -584,6 +591,8 @@ void build_v6_twiddles(double2 *tw) {
         tw[kTwInv + 256 + 2 * 64 + L] = cexp(L, 512);
         tw[kTwInv + 256 + 3 * 64 + L] = cexp(L + 64, 512);
         for (int r = 0; r < 8; ++r) tw[kTwPost + r * 64 + L] = cexp(L + 64 * r, 2048);   // zeta^-n
+        tw[kTwSig + L] = cexp(L, 2048);                             // zeta^-L
+        tw[kTwInvAs + L] = cexp(17 * L, 2048);                      // e^{-2 pi i L / 128} zeta^-L
     }
     for (int L = 0; L < 64; ++L) {
         const int g = L >> 3;

@@ -20,6 +20,10 @@ struct Cx {
 // [1028, 1540) post-twist zeta^-(L + 64 r) [8][64]
 constexpr int kTwInv = 516;
 constexpr int kTwPost = 1028;
+// [1540, 1604) zeta^-L, [1604, 1668) the inverse pass-A twiddle a times zeta^-L (cmux_v6's folded
+// post-twist)
+constexpr int kTwSig = 1540;
+constexpr int kTwInvAs = 1604;
 
 __device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
@@ -114,6 +118,9 @@ __device__ __forceinline__ void pass_dit_C(Cx (&x)[8]) {
     bf_fwd<true>(x[3], x[7], Cx{-h, h});
 }
 
+__device__ __forceinline__ Cx cmul(const Cx &a, const Cx &b) {
+    return Cx{fma_(a.re, b.re, -(a.im * b.im)), fma_(a.re, b.im, a.im * b.re)};
+}
 __device__ __forceinline__ Cx ld(const double2 *p) {
     const double2 v = *p;
     return Cx{v.x, v.y};
@@ -391,6 +398,17 @@ __device__ __forceinline__ int t7_src(int e) {
     if (e < kT7InvA) return kTwInv + ((e - kT7InvB) >> 3) * 64 + ((e - kT7InvB) & 7);
     if (e < kT7Post) return kTwInv + 256 + (e - kT7InvA);
     return kTwPost + (e - kT7Post);
+}
+
+// v6's compact table: as above up to inverse pass A, whose first twiddle is a zeta^-L, then the
+// lane factor zeta^-L [64] in place of the 8 KB post-twist table
+constexpr int kT8Sig = 576, kT8Words = 640;
+static_assert(kT8Sig == kT7Post, "v6 and v7 tables agree up to the post-twist");
+__device__ __forceinline__ int t8_src(int e) {
+    if (e < kT7InvA) return t7_src(e);
+    if (e < kT7InvA + 64) return kTwInvAs + (e - kT7InvA);
+    if (e < kT8Sig) return kTwInv + 256 + (e - kT7InvA);
+    return kTwSig + (e - kT8Sig);
 }
 
 __device__ __forceinline__ Tw4 tw7_fwdB(const double2 *t, int L) {
