@@ -172,13 +172,24 @@ def pass_dit(x, a, b, c, c2):
     return x
 
 
-def inv_dit(Z):
+def inv_dit(Z, folded=True):
+    """folded (the kernel since round 2): the post-twist zeta^-(L + 64 r) split into the lane
+    factor zeta^-L, applied to pass A's inputs (u inputs of its first butterflies directly, v
+    inputs through its first twiddle a zeta^-L), and the register factor e^{-2 pi i r / 32} on
+    its outputs; else the 8-entry post-twist table per lane."""
     tB, tA, post = inv_tables()
     one = np.ones(64)
     z = pass_dit(Z, one, one, one, one * np.exp(-1j * np.pi / 4))
     z = pass_dit(relayout(z, IDX_C, IDX_B), *(tB[:, k] for k in range(4)))
-    z = pass_dit(relayout(z, IDX_B, IDX_A), *(tA[:, k] for k in range(4)))
-    z = z * post
+    z = relayout(z, IDX_B, IDX_A)
+    if folded:
+        sig = np.exp(-1j * np.pi * np.arange(64) / 1024)
+        z[:, 0::2] = z[:, 0::2] * sig[:, None]
+        z = pass_dit(z, tA[:, 0] * sig, tA[:, 1], tA[:, 2], tA[:, 3])
+        z = z * np.exp(-2j * np.pi * np.arange(8) / 32)[None, :]
+    else:
+        z = pass_dit(z, *(tA[:, k] for k in range(4)))
+        z = z * post
     flat = relayout(z, IDX_A, np.arange(512))
     return np.concatenate([flat.real, flat.imag])
 
