@@ -53,6 +53,9 @@ HBM_PEAK_GBPS = 8000.0
 INV_FLOPS = 640 * 4 + 1664 * 12 + 512 * 6
 FLOPS_PER_CMUX = 4 * 2304 * 12 + 2 * INV_FLOPS + 2 * 4 * 512 * 7 + 2048 + 2048 * 3   # 198 656
 FLOPS_PER_BOOTSTRAP = 500 * FLOPS_PER_CMUX
+# the textbook count: 10 FLOP per non-trivial radix-2 butterfly (one complex multiply = 6, two
+# complex adds = 4) instead of the 6 FMAs = 12 the kernel issues; `roofline.frac_10flop`
+FLOPS_PER_CMUX_10 = 4 * 2304 * 10 + 2 * (640 * 4 + 1664 * 10 + 512 * 6) + 2 * 4 * 512 * 7 + 2048 + 2048 * 3  # 173 568
 FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (FMA = 2 FLOP) at the 2.4 GHz peak clock
 PEAK_CLOCK_MHZ = 2400.0
 
@@ -71,6 +74,8 @@ def parse():
     ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the sustained fp64 ceiling measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--parity-samples", type=int, default=128,
+                    help="outputs of the timed batch compared Torus32-for-Torus32 with the exact oracle")
     return ap.parse_args()
 
 
@@ -102,35 +107,76 @@ def cpu_threads():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(bk, ksk, rng, target_s):
-    """The optimized CPU port (oracle/cpu_fft.c) on the host threads this process may use
-    (OMP_NUM_THREADS, else its CPU affinity): ~target_s of work, plus a single-thread sample."""
+def cpu_share():
+    """What caps the CPU baseline's thread count on this host: OMP_NUM_THREADS (the GPU pool sets
+    it to each GPU's share of the host, 16), the cgroup CPU quota, the affinity mask; plus the
+    physical core count (unique (socket, core) pairs) for the full-socket extrapolation."""
+    out = {"omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        out["cgroup_cpu_quota"] = None if q[0] == "max" else float(q[0]) / float(q[1])
+    except (OSError, ValueError, IndexError):
+        out["cgroup_cpu_quota"] = None
+    cores, phys = set(), None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":")[1].strip()))
+    except OSError:
+        pass
+    out["physical_cores"] = len(cores) or None
+    return out
+
+
+def cpu_baseline(bk, ksk, inputs, gpu_out, target_s):
+    """The optimized CPU port (oracle/cpu_fft.c) on the SAME inputs as the timed GPU batch (the
+    batch repeated to fill ~target_s), on the threads this process may use (OMP_NUM_THREADS, else
+    its CPU affinity), plus a single-thread sample.  Its outputs are also compared word for word
+    with the GPU's outputs of that batch (the port is Torus32-identical to the exact oracle,
+    tests/test_cpu_baseline.py)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_ctypes as O
     fk = O.CpuFftKey(bk, ksk)
     threads = cpu_threads()
-    n = 500
+    a_a, a_b, b_a, b_b = inputs
+    B = a_a.shape[0]
+    g_a, g_b = gpu_out
 
-    def run(B, th):
-        a = rng.integers(-2**31, 2**31, (B, n), dtype=np.int64).astype(np.int32)
-        b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
+    def run(lo, hi, th):
         t0 = time.perf_counter()
-        fk.gate_batch("NAND", a, b, a[::-1].copy(), b[::-1].copy(), nthreads=th)
-        return time.perf_counter() - t0
+        r = fk.gate_batch("NAND", a_a[lo:hi], a_b[lo:hi], b_a[lo:hi], b_b[lo:hi], nthreads=th)
+        return time.perf_counter() - t0, r
 
-    run(threads, threads)                  # warm-up (thread team, key pages)
-    t1 = run(2 * threads, threads)         # rate estimate
-    B = max(threads, int(target_s / max(t1 / 2, 1e-3)) * threads)
-    t = run(B, threads)
-    run(1, 1)
-    single = min(run(4, 1) / 4 for _ in range(2))
-    out = {"value": B / t, "unit": "gate bootstraps/s", "cores": threads, "kind": "port",
-           "sample": f"{B} bootsNAND (random LWE inputs) on {threads} OpenMP threads, {t:.1f} s",
+    run(0, min(B, threads), threads)                  # warm-up (thread team, key pages)
+    t1, (c_a, c_b) = run(0, B, threads)               # the whole timed batch once
+    mismatches = int(np.sum(np.any(c_a != g_a, axis=1) | (c_b != g_b)))
+    reps = max(0, int(target_s / max(t1, 1e-3)) - 1)
+    t, n = t1, B
+    for _ in range(reps):                             # the same batch again, to fill the sample
+        dt, _ = run(0, B, threads)
+        t += dt
+        n += B
+    run(0, 1, 1)
+    single = min(run(0, 4, 1)[0] / 4 for _ in range(2))
+    share = cpu_share()
+    out = {"value": n / t, "unit": "gate bootstraps/s", "cores": threads, "kind": "port",
+           "sample": f"the timed GPU batch's {B} bootsNAND inputs, {n // B} pass(es) = {n} bootstraps on "
+                     f"{threads} OpenMP threads, {t:.1f} s",
            "engine": "optimized fp64-FFT port of the reference CPU path (oracle/cpu_fft.c; spqlios "
                      "algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to the exact oracle)",
+           "same_inputs_as_gpu": True, "outputs_vs_gpu": {"checked": B, "mismatches": mismatches},
            "single_core_ms_per_bootstrap": single * 1e3,
            "paper_single_core_ms_per_gate": 43.8,
-           "max_round_error": fk.max_round_error()}
+           "max_round_error": fk.max_round_error(),
+           "thread_cap": share,
+           "thread_cap_note": "threads = OMP_NUM_THREADS, which the GPU pool sets to each GPU's share of "
+                              "the host's CPUs (16 per GPU); nproc / affinity show the whole machine"}
+    if share.get("physical_cores"):
+        out["full_socket_extrapolation"] = {
+            "value": share["physical_cores"] * 1e3 / (single * 1e3), "cores": share["physical_cores"],
+            "note": "single-core rate x physical cores (linear; an upper bound, not measured)"}
     out.update(host_info())
     return out
 
@@ -207,6 +253,32 @@ def sample_clock(device, run_step, seconds=2.0):
     return {"mhz": samples[len(samples) // 2], "samples": len(samples)}
 
 
+def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
+    """Torus32 parity of the timed batch itself: `nsamp` of its outputs (launch seams, rounds and
+    a seeded random sample) against the exact CPU oracle (tests/oracle_ctypes.py, test-only
+    checker), max-reduced over the ranks."""
+    import shard
+    a_a, a_b, b_a, b_b = rec["inputs"]
+    g_a, g_b = rec["outputs"]
+    B = a_a.shape[0]
+    if B == 0 or nsamp <= 0:
+        return {"checked_per_rank": 0, "mismatches": 0}
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_ctypes as O
+    seams = [i for i in (0, 1, 63, 64, 127, 128, 255, 256, 257, 511, 512, 513, 767, 768, 1023, 1024, 1025,
+                         2047, 2048, 4095) if i < B] + [B - 1]
+    rng = np.random.default_rng(4242 + rank)
+    rest = rng.choice(B, min(B, max(0, nsamp - len(seams))), replace=False)
+    idx = np.unique(np.concatenate([np.array(seams, dtype=np.int64), rest.astype(np.int64)]))
+    ok = O.OracleKey(K.bk, K.ksk, use_ntt=True)
+    o_a, o_b = ok.gate_batch(gate, a_a[idx], a_b[idx], b_a[idx], b_b[idx])
+    bad = int(np.sum(np.any(g_a[idx] != o_a, axis=1) | (g_b[idx] != o_b)))
+    if world > 1:
+        bad = int(shard.max_over_ranks(float(bad), device=red_dev))
+    return {"checked_per_rank": int(len(idx)), "mismatches": bad, "vs": "exact CPU oracle (oracle/tfhe_oracle.c)",
+            "what": "outputs of the timed batch, Torus32 words (a[500], b)"}
+
+
 def main():
     args = parse()
     import torch
@@ -246,12 +318,12 @@ def main():
         r_a = torch.empty((B, 500), dtype=torch.int32, device="cuda")
         r_b = torch.empty(B, dtype=torch.int32, device="cuda")
         ctx.reserve(B)
-        return x, y, dev, r_a, r_b
+        return x, y, dev, r_a, r_b, (a_a, a_b, b_a, b_b)
 
     def timed(B, steps, warmup, profile=False):
         """W warmup + K timed steps of batch B, barrier + synchronize on both sides, max over
-        ranks; returns (elapsed_s, profile dict, truth_ok)."""
-        x, y, dev, r_a, r_b = make_batch(B)
+        ranks; returns (elapsed_s, profile dict, truth_ok, step, batch record)."""
+        x, y, dev, r_a, r_b, host_in = make_batch(B)
 
         def step():
             if B > 0:
@@ -278,13 +350,15 @@ def main():
             prof = ctx.profile_read()
             ctx.profile_enable(False)
         ok = None
+        out = (r_a.cpu().numpy(), r_b.cpu().numpy()) if B > 0 else None
         if args.gate == "NAND" and B > 0:
-            dec = K.decrypt(r_a.cpu().numpy(), r_b.cpu().numpy())
+            dec = K.decrypt(*out)
             ok = bool(np.array_equal(dec, 1 - (x & y)))
-        return el, prof, ok, step
+        return el, prof, ok, step, {"inputs": host_in, "outputs": out, "kernels": ctx.last_kernels()}
 
     B = args.batch
-    elapsed, prof, truth_ok, main_step = timed(B, args.steps, args.warmup, profile=True)
+    elapsed, prof, truth_ok, main_step, rec = timed(B, args.steps, args.warmup, profile=True)
+    parity = headline_parity(K, args.gate, rec, args.parity_samples, rank, world, red_dev)
 
     br_ms = prof["br_ms"] / max(1, prof["br_launches"])
     ks_ms = prof["ks_ms"] / max(1, prof["ks_launches"])
@@ -304,8 +378,12 @@ def main():
                    "key; the streaming model counts every ciphertext's key stream, served from L2"}
     if fft:
         tflops = B * FLOPS_PER_BOOTSTRAP / (br_ms * 1e-3) / 1e12
+        tflops10 = B * 500 * FLOPS_PER_CMUX_10 / (br_ms * 1e-3) / 1e12
         roof = {"bound": "valu-fp64", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tflops / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel, "kernel_ms": br_ms,
+                "frac": tflops / FP64_PEAK_TFLOPS, "flop_convention": "frac: 12 FLOP per radix-2 butterfly (the 6 "
+                "v_fma_f64 the kernel issues, FMA = 2); frac_10flop: the textbook 10",
+                "achieved_10flop": tflops10, "frac_10flop": tflops10 / FP64_PEAK_TFLOPS,
+                "traffic": traffic, "kernel": kernel, "kernel_ms": br_ms,
                 "keyswitch_ms": ks_ms, "flops_per_launch": B * FLOPS_PER_BOOTSTRAP,
                 "flops_per_cmux_step": FLOPS_PER_CMUX, "hbm": hbm}
     else:   # exact-NTT generations: integer VALU bound; report the key-stream view only
@@ -332,6 +410,8 @@ def main():
                    "parallelism": f"shard{world} (independent ciphertexts, no collective)"},
         "roofline": roof,
         "truth_table_ok": truth_ok,
+        "parity": parity,
+        "kernels": rec["kernels"],
         "engine": T.version(),
     }
 
@@ -367,7 +447,7 @@ def main():
         if b == B or b <= 0:
             continue
         steps = max(3, min(args.steps, int(200 / b) + 5)) if b < 64 else max(3, args.steps // 2)
-        el, pr, ok, _ = timed(b, steps, 1, profile=True)
+        el, pr, ok, _, _ = timed(b, steps, 1, profile=True)
         extras[str(b)] = {"value": shard.weak_scaling_value(b, world, steps, el), "ms_per_step": el / steps * 1e3,
                           "steps": steps, "kernel_ms": pr["br_ms"] / max(1, pr["br_launches"]),
                           "keyswitch_ms": pr["ks_ms"] / max(1, pr["ks_launches"]), "truth_table_ok": ok}
@@ -377,13 +457,14 @@ def main():
     if args.strong_batch > 0:
         lo, hi = shard.shard_range(args.strong_batch, rank, world)
         steps = max(3, args.steps // 2)
-        el, _, ok, _ = timed(hi - lo, steps, 1)
+        el, _, ok, _, _ = timed(hi - lo, steps, 1)
         line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
                           "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
                           "steps": steps, "truth_table_ok": ok}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(K.bk, K.ksk, np.random.default_rng(5), args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(K.bk, K.ksk, rec["inputs"], rec["outputs"], args.cpu_seconds)
+        parity["vs_cpu_port"] = line["cpu_baseline"]["outputs_vs_gpu"]
         line["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(line), flush=True)

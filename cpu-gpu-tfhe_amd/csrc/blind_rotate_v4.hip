@@ -352,6 +352,7 @@ hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const
     const int total = B * halves;
     // guard mode: 256 workgroups scan the flags (B = 1024: 15 -> ~4 us per launch)
     const int grid = gd.flags && total > kGuardGrid ? kGuardGrid : total;
+    trace_kernel(gd.flags ? "k_blind_rotate_v4(guard)" : "k_blind_rotate_v4");
     if (gd.flags)
         hipLaunchKernelGGL(k_blind_rotate_v4<1>, dim3(grid), dim3(kV4Threads), 0, s, v4_args(key), B, total, in[0],
                            in1, mu, u_a, u_b, gd);
@@ -369,6 +370,7 @@ hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, c
     const V4Guard gd = v4_guard(guard);
     const long total = (long)B * nrows;
     const long grid = gd.flags && total > kGuardGrid ? kGuardGrid : total < 0x7fffffffL ? total : 0x7fffffffL;
+    trace_kernel(gd.flags ? "k_blind_rotate_v4_rows(guard)" : "k_blind_rotate_v4_rows");
     if (gd.flags)
         hipLaunchKernelGGL(k_blind_rotate_v4_rows<1>, dim3((unsigned)grid), dim3(kV4Threads), 0, s, v4_args(key), B,
                            total, rows, wa, wb, mu, u_a, u_b, gd);
@@ -382,6 +384,7 @@ hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, 
                                         hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (iters < 0 || iters > kn) return hipErrorInvalidValue;
+    trace_kernel("k_blind_rotate_v4_debug");
     hipLaunchKernelGGL(k_blind_rotate_v4_debug, dim3(B), dim3(kV4Threads), 0, s, v4_args(key), iters, acc, bara);
     return hipGetLastError();
 }

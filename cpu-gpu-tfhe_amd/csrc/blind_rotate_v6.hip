@@ -681,9 +681,11 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
         const long n = total - base < chunk ? total - base : chunk;
         if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
+            trace_kernel("k_blind_rotate_v6p(paired,reg-rotation)");
             hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
                                v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
         } else {
+            trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6(reg-rotation)" : "k_blind_rotate_v6(lds-rotation)");
             if (v6_rreg(key, n))
                 hipLaunchKernelGGL((k_blind_rotate_v6<kV6Waves, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
                                    v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
@@ -704,6 +706,7 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
         if (n > 0x7fffffffL) return hipErrorInvalidValue;
+        trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6_rows(reg-rotation)" : "k_blind_rotate_v6_rows(lds-rotation)");
         if (v6_rreg(key, n))
             hipLaunchKernelGGL((k_blind_rotate_v6_rows<kV6Waves, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
                                v6_args(key, n, guard), B, base, rows, wa, wb, mu, u_a, u_b);
@@ -718,6 +721,7 @@ hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, 
                                         hipStream_t s) {
     if (B <= 0) return hipSuccess;
     if (iters < 0 || iters > kn || !key.bk_fft) return hipErrorInvalidValue;
+    trace_kernel(v6_rreg(key, B) ? "k_blind_rotate_v6_debug(reg-rotation)" : "k_blind_rotate_v6_debug(lds-rotation)");
     if (v6_rreg(key, B))
         hipLaunchKernelGGL(k_blind_rotate_v6_debug<true>, dim3(B), dim3(kV6Threads), 0, s, v6_args(key, 0), iters, acc,
                            bara);

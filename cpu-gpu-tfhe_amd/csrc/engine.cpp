@@ -14,6 +14,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "engine.h"
@@ -67,6 +68,22 @@ void build_ntt_tables(NttTables *t) {
     }
     t->crt_h = host_powmod(kQ[0] % kQ[1], kQ[1] - 2, kQ[1]);
     t->crt_hp = shoup(t->crt_h, kQ[1]);
+}
+
+// the calling thread's trace sink: the context of the batch entry point it is in (TraceScope)
+static thread_local std::string *g_trace = nullptr;
+void trace_kernel(const char *name) {
+    if (!g_trace) return;
+    const size_t n = strlen(name);
+    for (size_t p = 0; p < g_trace->size();) {   // once per name, in first-launch order
+        const size_t e = g_trace->find(',', p);
+        const size_t len = (e == std::string::npos ? g_trace->size() : e) - p;
+        if (len == n && g_trace->compare(p, n, name) == 0) return;
+        if (e == std::string::npos) break;
+        p = e + 1;
+    }
+    if (!g_trace->empty()) g_trace->push_back(',');
+    g_trace->append(name);
 }
 
 static std::atomic<int> g_br_version{-1};
@@ -170,6 +187,22 @@ struct TfheAmdContext {
     // sliced host batches (gate_batch_host_sliced): copy streams and their events
     hipStream_t copy_in = nullptr, copy_out = nullptr;
     hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out[2] = {nullptr, nullptr};
+    std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
+};
+
+// Collects the launches of one C-ABI batch call into its context's last_kernels; nested calls
+// (the host path calls the device path) keep the outermost scope's sink.
+struct TraceScope {
+    std::string *prev;
+    explicit TraceScope(TfheAmdContext *c) : prev(g_trace) {
+        if (!prev) {
+            c->last_kernels.clear();
+            g_trace = &c->last_kernels;
+        }
+    }
+    ~TraceScope() {
+        if (!prev) g_trace = nullptr;
+    }
 };
 
 #define HIPCHK(x)                                                                 \
@@ -478,6 +511,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
     HIPCHK(c->fence.acquire(s));
@@ -518,6 +552,7 @@ extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32
     if (!x_a || !x_b || !u_a || !u_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);   // guard flags live in the context's scratch
     if (rc) return rc;
     HIPCHK(c->fence.acquire(s));
@@ -538,6 +573,7 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     if (!x_a || !x_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
     HIPCHK(c->fence.acquire(s));
@@ -560,6 +596,7 @@ extern "C" int tfhe_amd_keyswitch_batch_dev(TfheAmdContext *c, int B, const int3
     if (!u_a || !u_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, u_a, u_b, nullptr, nullptr, 0, res_a, res_b, s));
     return TFHE_AMD_OK;
@@ -572,6 +609,7 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     if (!acc || (iters > 0 && !bara)) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     ProfScope ps(c, s, true);
     const int v = br_version();
 #ifdef TFHE_AMD_EXPERIMENTAL
@@ -667,6 +705,7 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     if (!c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
     if (host_slice() > 0 && B > host_slice()) {
@@ -715,6 +754,7 @@ static int single_input_host(TfheAmdContext *c, int op, int B, int32_t mu, const
     if (!in_a || !in_b || !out_a || !out_b) return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
     const int din = op == OP_KS ? kN : kn, dout = op == OP_WOKS ? kN : kn;
@@ -748,6 +788,10 @@ extern "C" int tfhe_amd_keyswitch_batch_host(TfheAmdContext *c, int B, const int
                                              int32_t *res_a, int32_t *res_b) {
     return single_input_host(c, OP_KS, B, 0, u_a, u_b, res_a, res_b);
 }
+
+// largest batch the host path runs unsliced, i.e. whose key-switch inputs are all in the scratch
+// afterwards (tfhe_api.cpp's variance bookkeeping rounds)
+int tfhe_amd_internal_unsliced_max() { return host_slice() > 0 ? host_slice() : 1 << 30; }
 
 // The extracted samples (key-switch inputs) of this context's last gate batch of at most one
 // round (unsliced host path), halves x B rows of kN words: the Tier-1 API derives the
@@ -789,6 +833,7 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
     if (!wires_a || !wires_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
     std::lock_guard<std::mutex> lk(c->mu);
     return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b, c->gstats);
 }
@@ -816,6 +861,14 @@ extern "C" int tfhe_amd_guard_stats(TfheAmdContext *c, double *max_distance, lon
     if (recomputed) *recomputed = h[0];
     if (reset) HIPCHK(hipMemset(c->gstats, 0, sizeof h));
     return TFHE_AMD_OK;
+}
+
+extern "C" int tfhe_amd_last_kernels(TfheAmdContext *c, char *buf, int cap) {
+    if (!c || !buf || cap <= 0) return TFHE_AMD_E_ARG;
+    const size_t n = std::min(c->last_kernels.size(), (size_t)cap - 1);
+    memcpy(buf, c->last_kernels.data(), n);
+    buf[n] = 0;
+    return (int)c->last_kernels.size();
 }
 
 extern "C" int tfhe_amd_select_kernel(int br_version) {

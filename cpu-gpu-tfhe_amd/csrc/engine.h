@@ -146,6 +146,10 @@ hipError_t launch_blind_rotate_v7_debug(const DeviceKey &key, int B, int iters, 
                                         const int32_t *bara, hipStream_t s);
 // which blind-rotation kernel runs: 0 = default (v6), 1..7 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();
+// Launch trace: every launcher names the kernel (and variant) it enqueues; a batch entry point of
+// the C ABI collects the names of its launches into its context (tfhe_amd_last_kernels), so a
+// smoke or bench run can say which kernels produced the results it checked.
+void trace_kernel(const char *name);
 // circuit level blind rotation with the selected kernel (rows variants of v4 / v5 / v6); the
 // default fp64 kernel runs guarded (flags: 2 words per row x instance)
 hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,

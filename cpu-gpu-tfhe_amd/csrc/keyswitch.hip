@@ -693,6 +693,8 @@ static void launch_ks5(const uint4 *w5, int count, const P &io, hipStream_t s) {
     const int split = ks5_split(mtiles);
     if (split > 1) hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
     const dim3 grid(mtiles * kKs5Nb * split);
+    trace_kernel(split == 8 ? "k_keyswitch_v5(int8-mfma,split8)" : split == 4 ? "k_keyswitch_v5(int8-mfma,split4)"
+                 : split == 2 ? "k_keyswitch_v5(int8-mfma,split2)" : "k_keyswitch_v5(int8-mfma)");
     switch (split) {
     case 8: hipLaunchKernelGGL((k_keyswitch_v5<P, 8, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
     case 4: hipLaunchKernelGGL((k_keyswitch_v5<P, 4, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
@@ -709,6 +711,7 @@ static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io,
         launch_ks5<P, 1>(w5, count, io, s);
         return;
     }
+    trace_kernel("k_keyswitch_v4");
     if (count <= ks_split_max()) {
         hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
         hipLaunchKernelGGL((k_keyswitch_v4<P, 2>), dim3(2 * 128 * groups), dim3(kKs4Threads), 0, s,
@@ -745,6 +748,7 @@ hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const Cir
     if (B <= 0 || nks <= 0) return hipSuccess;
     KsRows io{ks, u_a, u_b, wa, wb, B, nks};
     if ((long)B * nks <= ks_small_max()) {
+        trace_kernel("k_keyswitch_small");
         hipLaunchKernelGGL(k_keyswitch_small_init<KsRows>, dim3(B * nks), dim3(512), 0, s, io);
         if ((long)B * nks <= ks_unroll_max())
             hipLaunchKernelGGL((k_keyswitch_small<KsRows, kKsSmallI>), dim3(kKsSmallChunks, B * nks), dim3(512), 0, s,
@@ -786,6 +790,7 @@ hipError_t launch_circuit_linear(int B, int nlin, const CircLin *lin, int32_t *w
     if (B <= 0 || nlin <= 0) return hipSuccess;
     const size_t total = (size_t)nlin * B * (kn + 1);
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 65536);
+    trace_kernel("k_circuit_linear");
     hipLaunchKernelGGL(k_circuit_linear, dim3(blocks), dim3(256), 0, s, B, nlin, lin, wa, wb);
     return hipGetLastError();
 }
@@ -829,6 +834,7 @@ hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, con
     } else
 #endif
     if (B <= ks_small_max()) {
+        trace_kernel("k_keyswitch_small");
         KsPlain io{u_a, u_b, u2_a, u2_b, add_b, res_a, res_b, B};
         hipLaunchKernelGGL(k_keyswitch_small_init<KsPlain>, dim3(B), dim3(512), 0, s, io);
         if (B <= ks_unroll_max())

@@ -98,6 +98,7 @@ struct TfheAmdMulti {
 
 extern "C" int tfhe_amd_multi_destroy(TfheAmdMulti *m) {
     if (!m) return TFHE_AMD_OK;
+    { std::lock_guard<std::mutex> lk(m->mu); }   // a batch still running on it finishes first
     m->workers.clear();   // joins the threads
     for (auto *c : m->ctx)
         if (c) tfhe_amd_context_destroy(c);
@@ -198,48 +199,53 @@ extern "C" int tfhe_amd_multi_gate_batch_host(TfheAmdMulti *m, int gate, int B, 
 // tfhe_gpu_init registers a multi-device context for a cloud key; tfhe_gpu_boots_batch runs a
 // batch of one gate over it (falling back to the key's Tier-1 device when not registered).
 
+// Registered multi-contexts are shared: a batch holds its own reference for the whole call, so a
+// concurrent tfhe_gpu_init (re-registration) or key deletion only drops the registry's reference
+// and the last in-flight batch frees the contexts and joins the workers.
 static std::mutex g_multi_mu;
-static std::unordered_map<const void *, TfheAmdMulti *> g_multi;   // bkFFT -> multi-context
+static std::unordered_map<const void *, std::shared_ptr<TfheAmdMulti>> g_multi;   // bkFFT -> multi-context
+
+static std::shared_ptr<TfheAmdMulti> share_multi(TfheAmdMulti *m) {
+    return std::shared_ptr<TfheAmdMulti>(m, [](TfheAmdMulti *p) { tfhe_amd_multi_destroy(p); });
+}
 
 extern "C" int tfhe_gpu_init(const TFheGateBootstrappingCloudKeySet *bk, int device_mask) {
     if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
     TfheAmdMulti *m = nullptr;
     const int rc = tfhe_amd_multi_create(bk, device_mask, &m);
     if (rc != TFHE_AMD_OK) return rc;
-    TfheAmdMulti *old = nullptr;
+    std::shared_ptr<TfheAmdMulti> old;   // released outside the registry lock (may join workers)
     {
         std::lock_guard<std::mutex> lk(g_multi_mu);
         auto it = g_multi.find(bk->bkFFT);
-        if (it != g_multi.end()) old = it->second;
-        g_multi[bk->bkFFT] = m;
+        if (it != g_multi.end()) old = std::move(it->second);
+        g_multi[bk->bkFFT] = share_multi(m);
     }
-    tfhe_amd_multi_destroy(old);
     return TFHE_AMD_OK;
 }
 
 // drop the multi-context of a key being deleted (tfhe_api.cpp delete_* hooks)
 void tfhe_amd_internal_forget_multi(const void *bkfft) {
-    TfheAmdMulti *m = nullptr;
+    std::shared_ptr<TfheAmdMulti> m;   // in-flight batches keep their own reference
     {
         std::lock_guard<std::mutex> lk(g_multi_mu);
         auto it = g_multi.find(bkfft);
         if (it == g_multi.end()) return;
-        m = it->second;
+        m = std::move(it->second);
         g_multi.erase(it);
     }
-    tfhe_amd_multi_destroy(m);
 }
 
 extern "C" int tfhe_gpu_boots_batch(int gate, int32_t *res_a, int32_t *res_b, const int32_t *a_a, const int32_t *a_b,
                                     const int32_t *b_a, const int32_t *b_b, const int32_t *c_a, const int32_t *c_b,
                                     int B, const TFheGateBootstrappingCloudKeySet *bk) {
     if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
-    TfheAmdMulti *m = nullptr;
+    std::shared_ptr<TfheAmdMulti> m;   // held for the whole batch (see g_multi)
     {
         std::lock_guard<std::mutex> lk(g_multi_mu);
         auto it = g_multi.find(bk->bkFFT);
         if (it != g_multi.end()) m = it->second;
     }
-    if (m) return tfhe_amd_multi_gate_batch_host(m, gate, B, res_a, res_b, a_a, a_b, b_a, b_b, c_a, c_b);
+    if (m) return tfhe_amd_multi_gate_batch_host(m.get(), gate, B, res_a, res_b, a_a, a_b, b_a, b_b, c_a, c_b);
     return tfhe_amd_internal_tier1_batch(bk, gate, B, res_a, res_b, a_a, a_b, b_a, b_b, c_a, c_b);
 }

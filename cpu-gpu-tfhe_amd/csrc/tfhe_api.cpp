@@ -38,6 +38,7 @@ using namespace tfhe_amd;
 using namespace tfhe_amd::api;
 
 TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary);   // engine.cpp
+int tfhe_amd_internal_unsliced_max();                                 // engine.cpp
 
 // ------------------------------------------------------------------ numerics
 // numeric-functions.cu:11-77
@@ -791,12 +792,14 @@ EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a,
         memcpy(ba + (size_t)i * kn, b[i].a, kn * 4); bb[i] = b[i].b;
         if (c) { memcpy(ca + (size_t)i * kn, c[i].a, kn * 4); cb[i] = c[i].b; }
     }
-    // in rounds of at most 1024 gates (the unsliced host path), so that each round's key-switch
-    // inputs are still in the lane's scratch for the variance bookkeeping
+    // in rounds the host path runs unsliced (at most 1024, or TFHE_AMD_HOST_SLICE if smaller), so
+    // that each round's key-switch inputs are all still in the lane's scratch for the variance
+    // bookkeeping
     const int halves = gate == TFHE_GATE_MUX ? 2 : 1;
+    const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
     std::vector<int32_t> u;
-    for (int s0 = 0; s0 < B; s0 += 1024) {
-        const int n = B - s0 < 1024 ? B - s0 : 1024;
+    for (int s0 = 0; s0 < B; s0 += round) {
+        const int n = B - s0 < round ? B - s0 : round;
         const size_t o = (size_t)s0 * kn;
         int rc = tfhe_amd_gate_batch_host(l, gate, n, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
                                           c ? ca + o : nullptr, c ? cb + s0 : nullptr);

@@ -77,6 +77,7 @@ def _load():
     L.tfhe_amd_set_guard_threshold.argtypes = [ctypes.c_double]
     L.tfhe_amd_fp64_ceiling.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _VP, _VP]
     L.tfhe_amd_tier1_lane_count.argtypes = [_VP]
+    L.tfhe_amd_last_kernels.argtypes = [_VP, ctypes.c_char_p, ctypes.c_int]
     L.tfhe_amd_context_key_bytes.restype = ctypes.c_longlong
     L.tfhe_amd_context_key_bytes.argtypes = [_VP]
     L.tfhe_amd_multi_create_raw.argtypes = [_I32P, _I32P, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
@@ -447,6 +448,14 @@ class Context:
         d = ctypes.c_double(); r = ctypes.c_longlong()
         _check(lib.tfhe_amd_guard_stats(self.h, ctypes.byref(d), ctypes.byref(r), int(bool(reset))), "guard_stats")
         return d.value, r.value
+
+    def last_kernels(self):
+        """tfhe_amd_last_kernels: the kernels (and variants) the last batch call enqueued."""
+        buf = ctypes.create_string_buffer(1024)
+        n = lib.tfhe_amd_last_kernels(self.h, buf, 1024)
+        if n < 0:
+            raise TfheAmdError(f"last_kernels failed (rc={n})")
+        return [k for k in buf.value.decode().split(",") if k]
 
     def profile_enable(self, on=True):
         _check(lib.tfhe_amd_profile_enable(self.h, int(on)), "profile_enable")

@@ -182,6 +182,13 @@ int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32
  * cross-checks; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
 
+/* The kernels (with the variant the launch geometry picked, e.g. "k_blind_rotate_v6(reg-rotation)",
+ * "k_blind_rotate_v4(guard)", "k_keyswitch_v5(int8-mfma,split2)") that the context's last batch
+ * call enqueued, comma-separated in first-launch order, NUL-terminated into buf[cap].  Returns the
+ * full length (which may exceed cap - 1).  For smoke / bench reports of which kernels produced
+ * the checked outputs. */
+int tfhe_amd_last_kernels(TfheAmdContext *ctx, char *buf, int cap);
+
 /* Exactness guard of the default fp64 FFT blind rotation: every launch
  * measures, per ciphertext, the largest distance |c - rint(c)| of any rounded external-product
  * coefficient over its 500 steps; a ciphertext at or above the threshold (default 1/4; the
