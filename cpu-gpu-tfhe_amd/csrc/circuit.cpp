@@ -17,6 +17,9 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "engine.h"
@@ -44,24 +47,17 @@ struct Affine {          // W = (0, c) + s W[base]; base = -1: the trivial sampl
 
 }  // namespace
 
-struct TfheAmdCircuit {
-    std::vector<Node> nodes;           // one per wire
-    // compiled schedule
-    bool compiled = false;
-    struct Level { int row0, nrows, ks0, nks, lin0, nlin; };
-    std::vector<Level> levels;         // levels[0]: affine nodes over inputs only
-    std::vector<CircRow> rows;
-    std::vector<CircKs> ks;
-    std::vector<CircLin> lin;
-    int n_boot = 0, max_rows = 0;
-    // device copies (per device) and u scratch
+// Device state of a circuit for ONE executing context: the level tables on its device and the
+// extracted-sample scratch.  Contexts that run the same circuit at the same time (the shards of a
+// multi-device run, tfhe_amd_multi_circuit_run_*; several contexts on one GPU) each get their own.
+struct CircuitDevState {
     int dev = -1;
     void *d_tab = nullptr;
     int32_t *u_a = nullptr, *u_b = nullptr;
     uint32_t *u_flags = nullptr;   // exactness-guard flags, 2 words per u slot (engine.h Guard)
     size_t u_slots = 0;
     StreamFence fence;   // u scratch reuse across caller streams
-    ~TfheAmdCircuit() { release(); }
+    ~CircuitDevState() { release(); }
     void release() {
         if (dev >= 0) {
             (void)hipSetDevice(dev);
@@ -74,6 +70,21 @@ struct TfheAmdCircuit {
         if (u_flags) (void)hipFree(u_flags);
         d_tab = nullptr; u_a = nullptr; u_b = nullptr; u_flags = nullptr; u_slots = 0; dev = -1;
     }
+};
+
+struct TfheAmdCircuit {
+    std::vector<Node> nodes;           // one per wire
+    // compiled schedule
+    bool compiled = false;
+    struct Level { int row0, nrows, ks0, nks, lin0, nlin; };
+    std::vector<Level> levels;         // levels[0]: affine nodes over inputs only
+    std::vector<CircRow> rows;
+    std::vector<CircKs> ks;
+    std::vector<CircLin> lin;
+    int n_boot = 0, max_rows = 0;
+    // per executing context (keyed by the context): device tables + scratch
+    std::mutex mu;   // compile + the state map; runs on distinct contexts proceed concurrently
+    std::unordered_map<const void *, std::unique_ptr<CircuitDevState>> states;
 };
 
 namespace {
@@ -279,6 +290,7 @@ extern "C" int tfhe_amd_circuit_node(const TfheAmdCircuit *c, int w, int *kind, 
 extern "C" int tfhe_amd_circuit_info(TfheAmdCircuit *c, int *n_wires, int *n_gates, int *n_bootstraps,
                                      int *depth) {
     if (!c) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
     if (!c->compiled) {
         const int rc = compile(c);
         if (rc != TFHE_AMD_OK) return rc;
@@ -294,6 +306,7 @@ extern "C" int tfhe_amd_circuit_info(TfheAmdCircuit *c, int *n_wires, int *n_gat
 
 extern "C" int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_level, int cap) {
     if (!c) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
     if (!c->compiled) {
         const int rc = compile(c);
         if (rc != TFHE_AMD_OK) return rc;
@@ -303,21 +316,30 @@ extern "C" int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_lev
     return nl;
 }
 
-// wires_a [n_wires][B][500], wires_b [n_wires][B] on the context's device; input wires filled
+// wires_a [n_wires][B][500], wires_b [n_wires][B] on the context's device; input wires filled.
+// The circuit's structure must not change while runs are in flight (builders invalidate the
+// compiled schedule); runs on distinct contexts may overlap.
 int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
                                   TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb, uint32_t *guard_stats) {
-    if (!c->compiled) {
-        const int rc = compile(c);
-        if (rc != TFHE_AMD_OK) return rc;
+    CircuitDevState *st;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (!c->compiled) {
+            const int rc = compile(c);
+            if (rc != TFHE_AMD_OK) return rc;
+            c->states.clear();   // tables of an earlier schedule
+        }
+        auto &slot = c->states[ctx];
+        if (!slot) slot.reset(new CircuitDevState());
+        st = slot.get();
     }
-    (void)ctx;
-    if (c->dev != device || !c->d_tab) {
-        c->release();
-        c->dev = device;
+    if (st->dev != device || !st->d_tab) {
+        st->release();
+        st->dev = device;
         const size_t bytes = sizeof(CircRow) * c->rows.size() + sizeof(CircKs) * c->ks.size() +
                              sizeof(CircLin) * c->lin.size() + 64;
-        if (hipMalloc(&c->d_tab, bytes) != hipSuccess) return TFHE_AMD_E_NOMEM;
-        char *p = (char *)c->d_tab;
+        if (hipMalloc(&st->d_tab, bytes) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        char *p = (char *)st->d_tab;
         if (!c->rows.empty() && hipMemcpy(p, c->rows.data(), sizeof(CircRow) * c->rows.size(),
                                           hipMemcpyHostToDevice) != hipSuccess) return TFHE_AMD_E_HIP;
         p += sizeof(CircRow) * c->rows.size();
@@ -328,34 +350,34 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
                                          hipMemcpyHostToDevice) != hipSuccess) return TFHE_AMD_E_HIP;
     }
     const size_t need = (size_t)c->max_rows * B;
-    if (need > c->u_slots) {
+    if (need > st->u_slots) {
         (void)hipDeviceSynchronize();   // the old scratch may still be in use
-        if (c->u_a) (void)hipFree(c->u_a);
-        if (c->u_b) (void)hipFree(c->u_b);
-        if (c->u_flags) (void)hipFree(c->u_flags);
-        c->u_a = nullptr; c->u_b = nullptr; c->u_flags = nullptr; c->u_slots = 0;
-        if (hipMalloc(&c->u_a, sizeof(int32_t) * kN * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
-        if (hipMalloc(&c->u_b, sizeof(int32_t) * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
-        if (hipMalloc(&c->u_flags, sizeof(uint32_t) * 2 * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
-        c->u_slots = need;
+        if (st->u_a) (void)hipFree(st->u_a);
+        if (st->u_b) (void)hipFree(st->u_b);
+        if (st->u_flags) (void)hipFree(st->u_flags);
+        st->u_a = nullptr; st->u_b = nullptr; st->u_flags = nullptr; st->u_slots = 0;
+        if (hipMalloc(&st->u_a, sizeof(int32_t) * kN * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        if (hipMalloc(&st->u_b, sizeof(int32_t) * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        if (hipMalloc(&st->u_flags, sizeof(uint32_t) * 2 * need) != hipSuccess) return TFHE_AMD_E_NOMEM;
+        st->u_slots = need;
     }
-    if (c->fence.acquire(s) != hipSuccess) return TFHE_AMD_E_HIP;
-    const CircRow *d_rows = (const CircRow *)c->d_tab;
+    if (st->fence.acquire(s) != hipSuccess) return TFHE_AMD_E_HIP;
+    const CircRow *d_rows = (const CircRow *)st->d_tab;
     const CircKs *d_ks = (const CircKs *)(d_rows + c->rows.size());
     const CircLin *d_lin = (const CircLin *)(d_ks + c->ks.size());
     for (const auto &lv : c->levels) {
         if (lv.nrows) {
-            const Guard gd = guard_stats ? Guard{c->u_flags, guard_stats} : Guard{};
+            const Guard gd = guard_stats ? Guard{st->u_flags, guard_stats} : Guard{};
             const hipError_t e =
-                launch_blind_rotate_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, c->u_a, c->u_b, s, &gd);
+                launch_blind_rotate_rows(key, B, lv.nrows, d_rows + lv.row0, wa, wb, kE8, st->u_a, st->u_b, s, &gd);
             if (e != hipSuccess) return TFHE_AMD_E_HIP;
-            if (launch_keyswitch_rows(key, B, lv.nks, d_ks + lv.ks0, c->u_a, c->u_b, wa, wb, s) != hipSuccess)
+            if (launch_keyswitch_rows(key, B, lv.nks, d_ks + lv.ks0, st->u_a, st->u_b, wa, wb, s) != hipSuccess)
                 return TFHE_AMD_E_HIP;
         }
         if (lv.nlin && launch_circuit_linear(B, lv.nlin, d_lin + lv.lin0, wa, wb, s) != hipSuccess)
             return TFHE_AMD_E_HIP;
     }
-    return c->fence.done(s) == hipSuccess ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
+    return st->fence.done(s) == hipSuccess ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
 }
 
 // ------------------------------------------------------------------ integer builders

@@ -195,6 +195,145 @@ extern "C" int tfhe_amd_multi_gate_batch_host(TfheAmdMulti *m, int gate, int B, 
     return rc;
 }
 
+// Device-resident shards: slot i's shard (counts[i] gates) already lives on that slot's device;
+// the batch is enqueued on every slot (streams[i], or the slot context's own stream when streams or
+// streams[i] is NULL) and the call returns without waiting (tfhe_amd_multi_sync).  No PCIe in the
+// loop: the shards' inputs and results stay in each device's HBM.
+extern "C" int tfhe_amd_multi_gate_batch_dev(TfheAmdMulti *m, int gate, const int *counts, int32_t *const *res_a,
+                                             int32_t *const *res_b, const int32_t *const *ca_a,
+                                             const int32_t *const *ca_b, const int32_t *const *cb_a,
+                                             const int32_t *const *cb_b, const int32_t *const *cc_a,
+                                             const int32_t *const *cc_b, void *const *streams) {
+    if (!m || !counts || !res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
+    if (gate < TFHE_GATE_NAND || gate > TFHE_GATE_MUX) return TFHE_AMD_E_ARG;
+    if (gate == TFHE_GATE_MUX && (!cc_a || !cc_b)) return TFHE_AMD_E_ARG;
+    const int world = (int)m->ctx.size();
+    for (int r = 0; r < world; ++r)
+        if (counts[r] < 0) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(m->mu);
+    for (int r = 0; r < world; ++r) {
+        if (counts[r] == 0) continue;
+        const int rc = tfhe_amd_gate_batch_dev(m->ctx[r], gate, counts[r], res_a[r], res_b[r], ca_a[r], ca_b[r],
+                                               cb_a[r], cb_b[r], cc_a ? cc_a[r] : nullptr, cc_b ? cc_b[r] : nullptr,
+                                               streams ? streams[r] : nullptr);
+        if (rc != TFHE_AMD_OK) return rc;
+    }
+    return TFHE_AMD_OK;
+}
+
+// waits for every slot context's own stream
+extern "C" int tfhe_amd_multi_sync(TfheAmdMulti *m) {
+    if (!m) return TFHE_AMD_E_ARG;
+    int rc = TFHE_AMD_OK;
+    for (auto *c : m->ctx) {
+        const int x = tfhe_amd_sync(c);
+        if (x != TFHE_AMD_OK && rc == TFHE_AMD_OK) rc = x;
+    }
+    return rc;
+}
+
+// A circuit over the devices, device-resident: slot i evaluates counts[i] instances in its own
+// wire arrays wires_a[i] [n_wires][counts[i]][500], wires_b[i] [n_wires][counts[i]] (input wires
+// filled).  Enqueued on every slot, returns without waiting.
+extern "C" int tfhe_amd_multi_circuit_run_dev(TfheAmdMulti *m, TfheAmdCircuit *circ, const int *counts,
+                                              int32_t *const *wires_a, int32_t *const *wires_b,
+                                              void *const *streams) {
+    if (!m || !circ || !counts || !wires_a || !wires_b) return TFHE_AMD_E_ARG;
+    const int world = (int)m->ctx.size();
+    for (int r = 0; r < world; ++r)
+        if (counts[r] < 0 || (counts[r] > 0 && (!wires_a[r] || !wires_b[r]))) return TFHE_AMD_E_ARG;
+    int rc = tfhe_amd_circuit_info(circ, nullptr, nullptr, nullptr, nullptr);   // compile once, here
+    if (rc != TFHE_AMD_OK) return rc;
+    std::lock_guard<std::mutex> lk(m->mu);
+    for (int r = 0; r < world; ++r) {
+        if (counts[r] == 0) continue;
+        rc = tfhe_amd_circuit_run_dev(m->ctx[r], circ, counts[r], wires_a[r], wires_b[r],
+                                      streams ? streams[r] : nullptr);
+        if (rc != TFHE_AMD_OK) return rc;
+    }
+    return TFHE_AMD_OK;
+}
+
+namespace {
+
+// copies `nw` wires between the caller's host planes [nw][B][ld] (instance rows lo..lo+n) and a
+// device wire array [n_wires][n][ld], one 2-D copy per run of consecutive wire ids
+int copy_planes(int32_t *dev, const int *wires, int nw, int32_t *host, long long B, long long lo, int n, int ld,
+                bool to_device, hipStream_t s) {
+    for (int k0 = 0; k0 < nw;) {
+        int k1 = k0 + 1;
+        while (k1 < nw && wires[k1] == wires[k1 - 1] + 1) ++k1;
+        int32_t *d = dev + (size_t)wires[k0] * n * ld;
+        int32_t *h = host + ((size_t)k0 * B + lo) * ld;
+        const size_t dp = (size_t)n * ld * 4, hp = (size_t)B * ld * 4;
+        const hipError_t e = to_device ? hipMemcpy2DAsync(d, dp, h, hp, dp, k1 - k0, hipMemcpyHostToDevice, s)
+                                       : hipMemcpy2DAsync(h, hp, d, dp, dp, k1 - k0, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return TFHE_AMD_E_HIP;
+        k0 = k1;
+    }
+    return TFHE_AMD_OK;
+}
+
+}  // namespace
+
+// A circuit over the devices from host memory: B instances split into contiguous shards (as
+// tfhe_amd_shard_range); every device copies in its shard of the n_in input wires
+// (in_a [n_in][B][500], in_b [n_in][B]: plane k is wire in_wires[k]), evaluates the circuit in its
+// own HBM wire arrays and copies back its shard of the n_out wires out_wires into out_a
+// [n_out][B][500], out_b [n_out][B].  Synchronous.  Generalizes the reference's matrix-vector
+// product over a device (BOOTS_matrixMultiplication, gpuParallel/main.cu:2342-2462; row layout
+// matrixUtility.cu:65-96) to all of a node's GPUs from one host process.
+extern "C" int tfhe_amd_multi_circuit_run_host(TfheAmdMulti *m, TfheAmdCircuit *circ, int B, int n_in,
+                                               const int *in_wires, const int32_t *in_a, const int32_t *in_b,
+                                               int n_out, const int *out_wires, int32_t *out_a, int32_t *out_b) {
+    if (!m || !circ || B < 0 || n_in < 0 || n_out < 0) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if ((n_in && (!in_wires || !in_a || !in_b)) || (n_out && (!out_wires || !out_a || !out_b))) return TFHE_AMD_E_ARG;
+    int n_wires = 0;
+    int rc = tfhe_amd_circuit_info(circ, &n_wires, nullptr, nullptr, nullptr);   // compile once, here
+    if (rc != TFHE_AMD_OK) return rc;
+    for (int k = 0; k < n_in; ++k)
+        if (in_wires[k] < 0 || in_wires[k] >= n_wires) return TFHE_AMD_E_ARG;
+    for (int k = 0; k < n_out; ++k)
+        if (out_wires[k] < 0 || out_wires[k] >= n_wires) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(m->mu);
+    const int world = (int)m->ctx.size();
+    std::vector<int> used;
+    for (int r = 0; r < world; ++r) {
+        long long lo, hi;
+        tfhe_amd_shard_range(B, r, world, &lo, &hi);
+        if (hi == lo) continue;
+        const int n = (int)(hi - lo);
+        TfheAmdContext *c = m->ctx[r];
+        const int dev = m->devices[r];
+        m->workers[r]->submit([=]() -> int {
+            if (hipSetDevice(dev) != hipSuccess) return TFHE_AMD_E_HIP;
+            hipStream_t s = (hipStream_t)tfhe_amd_context_stream(c);
+            int32_t *wa = nullptr, *wb = nullptr;
+            if (hipMalloc(&wa, sizeof(int32_t) * (size_t)n_wires * n * kn) != hipSuccess) return TFHE_AMD_E_NOMEM;
+            if (hipMalloc(&wb, sizeof(int32_t) * (size_t)n_wires * n) != hipSuccess) {
+                (void)hipFree(wa);
+                return TFHE_AMD_E_NOMEM;
+            }
+            int x = copy_planes(wa, in_wires, n_in, const_cast<int32_t *>(in_a), B, lo, n, kn, true, s);
+            if (!x) x = copy_planes(wb, in_wires, n_in, const_cast<int32_t *>(in_b), B, lo, n, 1, true, s);
+            if (!x) x = tfhe_amd_circuit_run_dev(c, circ, n, wa, wb, s);
+            if (!x) x = copy_planes(wa, out_wires, n_out, out_a, B, lo, n, kn, false, s);
+            if (!x) x = copy_planes(wb, out_wires, n_out, out_b, B, lo, n, 1, false, s);
+            if (hipStreamSynchronize(s) != hipSuccess && !x) x = TFHE_AMD_E_HIP;
+            (void)hipFree(wa);
+            (void)hipFree(wb);
+            return x;
+        });
+        used.push_back(r);
+    }
+    for (int r : used) {
+        const int x = m->workers[r]->wait();
+        if (x != TFHE_AMD_OK && rc == TFHE_AMD_OK) rc = x;
+    }
+    return rc;
+}
+
 // ------------------------------------------------------------------ SURVEY.md §8(b) Tier-2 names
 // tfhe_gpu_init registers a multi-device context for a cloud key; tfhe_gpu_boots_batch runs a
 // batch of one gate over it (falling back to the key's Tier-1 device when not registered).

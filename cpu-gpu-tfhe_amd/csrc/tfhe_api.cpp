@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -515,12 +517,40 @@ EXPORT int bootsSymDecrypt(const LweSample *sample, const TFheGateBootstrappingS
 
 static std::atomic<int> g_default_device{0};
 
+// One pending single-gate call of the coalescing queue (below).
+struct Tier1Req {
+    int gate;
+    LweSample *r;
+    const LweSample *a, *b, *c;
+    bool done = false;
+    int rc = TFHE_AMD_OK;
+};
+
+// Coalescing queue of the Tier-1 gates of one key ("per-thread streams or a
+// batching queue").  The reference's CPU callers enter single gates from OpenMP teams
+// (Cipher.cpp:83-120, cloud.cpp:389-395); one B = 1 launch per call would occupy 2 waves of one
+// CU each, and a process has only 4 hardware queues.  Here a call enqueues its gate; whichever
+// waiting thread finds no batch running becomes the leader, takes every pending gate (grouped by
+// gate kind) and runs them as one batch per kind on its own lane, while the gates that arrive
+// meanwhile queue up for the next batch (group commit).  A lone thread is its own leader at once:
+// its B = 1 latency is the plain path's.  Once concurrency has been seen (the last batch held
+// more than one gate) the leader waits at most `window` for as many gates as that batch held.
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable done_cv, arrive_cv;
+    std::vector<Tier1Req *> pending;
+    bool busy = false;
+    size_t last_batch = 1;
+    long long batches = 0, gates = 0, largest = 0;
+};
+
 struct KeyEntry {
     uint64_t id;
     const LweKeySwitchKey *ks = nullptr;
     TfheAmdContext *primary = nullptr;
     std::vector<TfheAmdContext *> lanes;
     std::mutex mu;
+    Coalescer q;
 };
 static std::mutex g_reg_mu;
 static std::unordered_map<const void *, std::shared_ptr<KeyEntry>> g_reg;   // bkFFT or KSK -> entry
@@ -723,15 +753,138 @@ EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const Lwe
 
 // ------------------------------------------------------------------ gates
 
+// TFHE_AMD_TIER1_COALESCE=0: every thread runs its own B = 1 batches on its own lane (no queue);
+// TFHE_AMD_TIER1_WINDOW_US: the leader's wait for stragglers (default 50 us)
+static bool coalesce_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("TFHE_AMD_TIER1_COALESCE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+static int coalesce_window_us() {
+    static const int v = [] {
+        const char *e = getenv("TFHE_AMD_TIER1_WINDOW_US");
+        return e ? std::max(0, atoi(e)) : 50;
+    }();
+    return v;
+}
+
+// Runs one batch of queued gates on lane l: per gate kind one host batch (inputs staged before
+// anything is written, so a result may alias any input of its own call), then each output's
+// current_variance from its key-switch input, as the single-gate path.
+static void run_tier1_batch(TfheAmdContext *l, const LweKeySwitchKey *ks, const std::vector<Tier1Req *> &batch) {
+    std::vector<Tier1Req *> group;
+    std::vector<int32_t> buf, u;
+    std::vector<bool> taken(batch.size(), false);
+    for (size_t i0 = 0; i0 < batch.size(); ++i0) {
+        if (taken[i0]) continue;
+        const int gate = batch[i0]->gate;
+        group.clear();
+        for (size_t i = i0; i < batch.size(); ++i)
+            if (!taken[i] && batch[i]->gate == gate) {
+                taken[i] = true;
+                group.push_back(batch[i]);
+            }
+        const int n = (int)group.size();
+        const bool mux = gate == TFHE_GATE_MUX;
+        const size_t A = (size_t)n * kn;
+        buf.resize(4 * A + 4 * (size_t)n);
+        int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
+        int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
+        for (int i = 0; i < n; ++i) {
+            const Tier1Req *q = group[i];
+            memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
+            memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
+            if (mux) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
+        }
+        // one unsliced round at a time, so that its key-switch inputs are still in the scratch
+        const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
+        for (int s0 = 0; s0 < n; s0 += round) {
+            const int m = std::min(round, n - s0);
+            const size_t o = (size_t)s0 * kn;
+            const int rc = tfhe_amd_gate_batch_host(l, gate, m, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
+                                                    mux ? ca + o : nullptr, mux ? cb + s0 : nullptr);
+            if (rc != TFHE_AMD_OK) {
+                for (int i = s0; i < n; ++i) group[i]->rc = rc;
+                break;
+            }
+            ks_input_of_last(l, m, mux ? 2 : 1, u);
+            for (int i = 0; i < m; ++i) {
+                Tier1Req *q = group[s0 + i];
+                memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
+                q->r->b = rb[s0 + i];
+                q->r->current_variance = ks_variance(ks, u.data() + (size_t)i * kN);
+            }
+        }
+    }
+}
+
 static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b, const LweSample *c,
                   const TFheGateBootstrappingCloudKeySet *bk) {
     TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
-    check(tfhe_amd_gate_batch_host(l, gate, 1, r->a, &r->b, a->a, &a->b, b->a, &b->b, c ? c->a : nullptr,
-                                   c ? &c->b : nullptr),
-          "gate");
-    std::vector<int32_t> u;   // every gate ends in lweKeySwitch (boot-gates.cu:98-448)
-    ks_input_of_last(l, 1, gate == TFHE_GATE_MUX ? 2 : 1, u);
-    r->current_variance = ks_variance(bk->bkFFT->ks, u.data());
+    if (!coalesce_enabled()) {
+        check(tfhe_amd_gate_batch_host(l, gate, 1, r->a, &r->b, a->a, &a->b, b->a, &b->b, c ? c->a : nullptr,
+                                       c ? &c->b : nullptr),
+              "gate");
+        std::vector<int32_t> u;   // every gate ends in lweKeySwitch (boot-gates.cu:98-448)
+        ks_input_of_last(l, 1, gate == TFHE_GATE_MUX ? 2 : 1, u);
+        r->current_variance = ks_variance(bk->bkFFT->ks, u.data());
+        return;
+    }
+    std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
+    Coalescer &q = e->q;
+    Tier1Req req{gate, r, a, b, c};
+    std::unique_lock<std::mutex> lk(q.mu);
+    q.pending.push_back(&req);
+    q.arrive_cv.notify_one();
+    while (!req.done) {
+        if (q.busy) {
+            q.done_cv.wait(lk);
+            continue;
+        }
+        q.busy = true;   // this thread leads the next batch
+        if (q.last_batch > 1 && q.pending.size() < q.last_batch && coalesce_window_us() > 0) {
+            const size_t want = q.last_batch;
+            q.arrive_cv.wait_for(lk, std::chrono::microseconds(coalesce_window_us()),
+                                 [&] { return q.pending.size() >= want; });
+        }
+        std::vector<Tier1Req *> batch;
+        batch.swap(q.pending);
+        lk.unlock();
+        run_tier1_batch(l, bk->bkFFT->ks, batch);
+        lk.lock();
+        for (Tier1Req *x : batch) x->done = true;
+        q.last_batch = batch.size();
+        q.batches += 1;
+        q.gates += (long long)batch.size();
+        q.largest = std::max(q.largest, (long long)batch.size());
+        q.busy = false;
+        q.done_cv.notify_all();
+    }
+    lk.unlock();
+    check(req.rc, "gate");
+}
+
+EXPORT int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches,
+                                      long long *gates, long long *largest, int reset) {
+    if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
+    std::shared_ptr<KeyEntry> e;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find(bk->bkFFT);
+        if (it != g_reg.end()) e = it->second;
+    }
+    long long b = 0, g = 0, m = 0;
+    if (e) {
+        std::lock_guard<std::mutex> lk(e->q.mu);
+        b = e->q.batches; g = e->q.gates; m = e->q.largest;
+        if (reset) e->q.batches = e->q.gates = e->q.largest = 0;
+    }
+    if (batches) *batches = b;
+    if (gates) *gates = g;
+    if (largest) *largest = m;
+    return TFHE_AMD_OK;
 }
 
 EXPORT void bootsNAND(LweSample *r, const LweSample *a, const LweSample *b, const TFheGateBootstrappingCloudKeySet *bk) { gate1(TFHE_GATE_NAND, r, a, b, nullptr, bk); }

@@ -11,7 +11,11 @@ gpuParallel/main.cu:2342-2462; Cannon's algorithm :2590-2645) on one GPU.  Here:
   instances of that circuit, so every level is one launch over (gates x rows);
 * rows are sharded contiguously over ranks (shard.shard_range); rows are independent, so
   there is no collective on the data path — each rank decrypts / checks its own rows and only
-  the timing is reduced (max over ranks).  Keys are replicated per GPU.
+  the timing is reduced (max over ranks).  Keys are replicated per GPU;
+* or, from ONE host process: `run_rows_multi` hands all rows to the library's multi-device
+  circuit run (tfhe_amd_multi_circuit_run_host, csrc/multi.cpp), which shards them over the
+  devices of a MultiContext (one worker thread and key replica per device), the way a C++ host
+  such as the reference's cloud.cpp would drive a node.
 """
 import numpy as np
 
@@ -73,3 +77,30 @@ def run_rows_gpu(T, torch, ctx, keyset, C, a_w, x_w, y_w, A_rows, x_vec, nbits, 
     ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
     y = T.int_of([keyset.decrypt(ha[w], hb[w]) for w in y_w])
     return y, float(np.median(times))
+
+
+def encrypt_inputs(T, keyset, a_wires, x_wires, A_rows, x_vec, nbits, rng):
+    """(input wire ids, in_a [n_in][B][500], in_b [n_in][B]) for the multi-device host API"""
+    bits = instance_inputs(T, a_wires, x_wires, A_rows, x_vec, nbits)
+    wires = sorted(bits)
+    B = A_rows.shape[0]
+    in_a = np.empty((len(wires), B, 500), np.int32)
+    in_b = np.empty((len(wires), B), np.int32)
+    for k, w in enumerate(wires):
+        in_a[k], in_b[k] = keyset.encrypt(bits[w], rng)
+    return wires, in_a, in_b
+
+
+def run_rows_multi(T, multi, keyset, C, a_w, x_w, y_w, A_rows, x_vec, nbits, rng, extra_out=()):
+    """All rows through one MultiContext (rows sharded over its device slots inside the library):
+    (y [B], seconds, {wire: (a [B][500], b [B])} for the extra output wires, the encrypted inputs)."""
+    import time
+    wires, in_a, in_b = encrypt_inputs(T, keyset, a_w, x_w, A_rows, x_vec, nbits, rng)
+    outs = list(y_w) + list(extra_out)
+    B = A_rows.shape[0]
+    t0 = time.perf_counter()
+    out_a, out_b = multi.circuit_host(C, B, wires, in_a, in_b, outs)
+    dt = time.perf_counter() - t0
+    y = T.int_of([keyset.decrypt(out_a[k], out_b[k]) for k in range(len(y_w))])
+    extra = {w: (out_a[len(y_w) + k], out_b[len(y_w) + k]) for k, w in enumerate(extra_out)}
+    return y, dt, extra, (wires, in_a, in_b)

@@ -512,6 +512,59 @@ class MultiContext:
                                                   _p(None if cc_b is None else i32(cc_b))), "multi_gate_batch_host")
         return r_a, r_b
 
+    def gate_dev(self, gate, shards, streams=None):
+        """tfhe_amd_multi_gate_batch_dev: shards[i] = (res_a, res_b, ca_a, ca_b, cb_a, cb_b[, cc_a, cc_b])
+        int32 tensors on slot i's device (the shard of that slot; may be empty).  Enqueued on
+        every slot; call sync()."""
+        g = GATES[gate] if isinstance(gate, str) else int(gate)
+        k = len(self.devices)
+        if len(shards) != k:
+            raise TfheAmdError(f"need {k} shards, got {len(shards)}")
+        counts = (ctypes.c_int * k)()
+        arrs = [(_VP * k)() for _ in range(8)]
+        for i, sh in enumerate(shards):
+            B = sh[2].shape[0]
+            counts[i] = B
+            shapes = [(B, n_lwe), (B,)] * (4 if g == GATES["MUX"] else 3)
+            for j, t in enumerate(sh[:len(shapes)]):
+                if not t.is_cuda or t.dtype != torch.int32 or not t.is_contiguous() or tuple(t.shape) != shapes[j]:
+                    raise TfheAmdError(f"shard {i} tensor {j}: need a contiguous int32 GPU tensor {shapes[j]}")
+                if t.device.index is not None and t.device.index != self.devices[i]:
+                    raise TfheAmdError(f"shard {i} tensor {j} is on cuda:{t.device.index}, slot device {self.devices[i]}")
+                arrs[j][i] = t.data_ptr()
+        st = None
+        if streams is not None:
+            st = (_VP * k)(*[s for s in streams])
+        cc = (arrs[6], arrs[7]) if g == GATES["MUX"] else (None, None)
+        _check(lib.tfhe_amd_multi_gate_batch_dev(self.h, g, counts, arrs[0], arrs[1], arrs[2], arrs[3], arrs[4],
+                                                 arrs[5], cc[0], cc[1], st), "multi_gate_batch_dev")
+
+    def sync(self):
+        _check(lib.tfhe_amd_multi_sync(self.h), "multi_sync")
+
+    def circuit_host(self, circ, B, in_wires, in_a, in_b, out_wires):
+        """tfhe_amd_multi_circuit_run_host: the B instances sharded over the devices; in_a [n_in][B][500],
+        in_b [n_in][B] for the wires in_wires -> (out_a [n_out][B][500], out_b [n_out][B])."""
+        in_a = i32(in_a); in_b = i32(in_b)
+        n_in, n_out = len(in_wires), len(out_wires)
+        if in_a.shape != (n_in, B, n_lwe) or in_b.shape != (n_in, B):
+            raise TfheAmdError(f"inputs: need [{n_in}][{B}][500] / [{n_in}][{B}], got {in_a.shape} / {in_b.shape}")
+        out_a = np.zeros((n_out, B, n_lwe), np.int32); out_b = np.zeros((n_out, B), np.int32)
+        _check(lib.tfhe_amd_multi_circuit_run_host(self.h, circ.h, int(B), n_in, _ids(in_wires), _p(in_a), _p(in_b),
+                                                   n_out, _ids(out_wires), _p(out_a), _p(out_b)),
+               "multi_circuit_run_host")
+        return out_a, out_b
+
+    def circuit_dev(self, circ, shards, streams=None):
+        """tfhe_amd_multi_circuit_run_dev: shards[i] = (wires_a [n_wires][B_i][500], wires_b [n_wires][B_i])
+        on slot i's device.  Enqueued on every slot; call sync()."""
+        k = len(self.devices)
+        counts = (ctypes.c_int * k)(*[int(sh[0].shape[1]) for sh in shards])
+        wa = (_VP * k)(*[sh[0].data_ptr() for sh in shards])
+        wb = (_VP * k)(*[sh[1].data_ptr() for sh in shards])
+        st = None if streams is None else (_VP * k)(*streams)
+        _check(lib.tfhe_amd_multi_circuit_run_dev(self.h, circ.h, counts, wa, wb, st), "multi_circuit_run_dev")
+
     def guard_stats(self, reset=False):
         """per device slot: (largest rounding distance, ciphertexts recomputed exactly)"""
         out = []
@@ -561,6 +614,12 @@ lib.tfhe_amd_circuit_neg.argtypes = [_VP, ctypes.c_int, _IP, _IP]
 lib.tfhe_amd_circuit_abs.argtypes = [_VP, ctypes.c_int, _IP, _IP]
 lib.tfhe_amd_circuit_divu.argtypes = [_VP, ctypes.c_int, _IP, _IP, _IP, _IP]
 lib.tfhe_amd_circuit_div.argtypes = [_VP, ctypes.c_int, _IP, _IP, _IP]
+_VPP = ctypes.POINTER(_VP)
+lib.tfhe_amd_multi_gate_batch_dev.argtypes = [_VP, ctypes.c_int, _IP] + [_VPP] * 9
+lib.tfhe_amd_multi_sync.argtypes = [_VP]
+lib.tfhe_amd_multi_circuit_run_dev.argtypes = [_VP, _VP, _IP, _VPP, _VPP, _VPP]
+lib.tfhe_amd_multi_circuit_run_host.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _IP, _I32P, _I32P, ctypes.c_int,
+                                                _IP, _I32P, _I32P]
 CMP = {"GT": 0, "GE": 1, "LT": 2, "LE": 3, "EQ": 4, "NE": 5}
 for _f in ("add", "sub", "add_prefix", "mul"):
     getattr(lib, "tfhe_amd_circuit_" + _f).argtypes = (

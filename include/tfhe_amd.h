@@ -51,6 +51,7 @@ enum {
 };
 
 typedef struct TfheAmdContext TfheAmdContext;
+typedef struct TfheAmdCircuit TfheAmdCircuit;
 
 /* Device context = the key material of one cloud key on one GPU: the bootstrapping key in
  * the kernels' transform domains (converted on the device from the coefficient-domain key) and the
@@ -140,6 +141,29 @@ TfheAmdContext *tfhe_amd_multi_context(TfheAmdMulti *m, int i);
 int tfhe_amd_multi_gate_batch_host(TfheAmdMulti *m, int gate, int B, int32_t *res_a, int32_t *res_b,
                                    const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
                                    const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b);
+/* Device-resident shards (no PCIe in the loop): slot i's shard of counts[i] gates lives on slot
+ * i's device (arrays of per-slot device pointers, SoA as tfhe_amd_gate_batch_dev; cc_* for MUX
+ * only, may be NULL otherwise); enqueued on streams[i] (NULL array or entry = the slot context's
+ * own stream) and returns without waiting. */
+int tfhe_amd_multi_gate_batch_dev(TfheAmdMulti *m, int gate, const int *counts, int32_t *const *res_a,
+                                  int32_t *const *res_b, const int32_t *const *ca_a, const int32_t *const *ca_b,
+                                  const int32_t *const *cb_a, const int32_t *const *cb_b,
+                                  const int32_t *const *cc_a, const int32_t *const *cc_b, void *const *streams);
+/* waits for the own stream of every slot context */
+int tfhe_amd_multi_sync(TfheAmdMulti *m);
+/* A circuit (below) over the devices, device-resident: slot i evaluates counts[i] instances in its
+ * own wire arrays [n_wires][counts[i]][500] / [n_wires][counts[i]] (input wires filled); enqueued,
+ * returns without waiting. */
+int tfhe_amd_multi_circuit_run_dev(TfheAmdMulti *m, TfheAmdCircuit *circ, const int *counts,
+                                   int32_t *const *wires_a, int32_t *const *wires_b, void *const *streams);
+/* The same from host memory, synchronous: B instances in contiguous shards (tfhe_amd_shard_range);
+ * in_a [n_in][B][500], in_b [n_in][B] hold the input wires in_wires[k]; each device copies in its
+ * shard, evaluates in its own HBM and copies its shard of the wires out_wires[k] back into
+ * out_a [n_out][B][500], out_b [n_out][B].  The reference's matrix-vector product
+ * (BOOTS_matrixMultiplication, gpuParallel/main.cu:2342-2462) over every GPU of a node. */
+int tfhe_amd_multi_circuit_run_host(TfheAmdMulti *m, TfheAmdCircuit *circ, int B, int n_in, const int *in_wires,
+                                    const int32_t *in_a, const int32_t *in_b, int n_out, const int *out_wires,
+                                    int32_t *out_a, int32_t *out_b);
 /* shard [lo, hi) of `total` gates for rank of world */
 int tfhe_amd_shard_range(long long total, int rank, int world, long long *lo, long long *hi);
 
@@ -160,6 +184,16 @@ int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const 
 /* Number of per-thread lanes (stream + scratch) the Tier-1 API holds for this cloud key;
  * a thread's lanes are released when it exits (0 if the key has no device context). */
 int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
+
+/* Concurrent Tier-1 gate calls on one key are coalesced: a calling thread enqueues its gate; the
+ * first waiting thread that finds no batch running takes every pending gate and runs them as one
+ * batch per gate kind on its lane, while later calls queue for the next batch (a lone thread runs
+ * its gate at once, B = 1).  Results, aliasing and current_variance are as for a lone call.
+ * env TFHE_AMD_TIER1_COALESCE=0 disables the queue (per-thread B = 1 launches);
+ * TFHE_AMD_TIER1_WINDOW_US (default 50) bounds a leader's wait for stragglers.
+ * queue_stats: batches run, gates they held, the largest batch (reset = 1 zeroes them). */
+int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches, long long *gates,
+                               long long *largest, int reset);
 
 /* Device selection for the Tier-1 (single-gate) API: the GPU used by the cached
  * context of every cloud key (default 0). */
@@ -219,7 +253,6 @@ int tfhe_amd_fp64_ceiling(int device, int waves_per_simd, double seconds, double
  * two-gate case).  NOT / COPY / CONST cost no bootstrap: they are folded into the gates that
  * read them (and also written to their own wires).
  * Builders return the new wire id (>= 0) or a negative TFHE_AMD_E* code. */
-typedef struct TfheAmdCircuit TfheAmdCircuit;
 int tfhe_amd_circuit_create(TfheAmdCircuit **out);
 int tfhe_amd_circuit_destroy(TfheAmdCircuit *c);
 /* `count` fresh input wires; returns the first id */

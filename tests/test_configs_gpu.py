@@ -139,6 +139,47 @@ def test_config5_matvec_rows_64x64_16bit(ctx, keyset, rng):
     assert np.array_equal(y, (A.astype(object) @ xv.astype(object)).astype(np.int64))
 
 
+def test_config5_matvec_64x64_16bit_all_rows_multi_device(okey, keyset, rng):
+    """configs[4] in full: all 64 rows of y = A x (64 x 64, 16-bit) from one host process through
+    the library's multi-device circuit run (tfhe_amd_multi_circuit_run_host), the rows sharded over
+    the device slots — every visible GPU, or two contexts on device 0 of a one-GPU box.  Every row
+    decrypts to the integer product; the level-1 partial products (AND rows of input bits) of a
+    sample of rows, both shards' seam included, equal the oracle's bootsAND word for word."""
+    torch = _torch()
+    n_dev = torch.cuda.device_count()
+    slots = list(range(n_dev)) if n_dev > 1 else [0, 0]
+    cols, nbits, R = 64, 16, 64
+    C, a_w, x_w, y_w = matvec.build(T, cols, nbits)
+    A = rng.integers(0, 2**nbits, (R, cols))
+    A[0] = 2**nbits - 1
+    xv = rng.integers(0, 2**nbits, cols)
+    xv[:8] = 2**nbits - 1
+    inputs = set(a_w[0] + x_w[0])
+    ands = []   # AND rows whose inputs are both input wires
+    for w in range(C.info()["wires"]):
+        kind, gate, _, _, ins = C.node(w)
+        if kind == 1 and gate == T.GATES["AND"] and ins[0] in inputs and ins[1] in inputs:
+            ands.append((w, ins[0], ins[1]))
+        if len(ands) == 6:
+            break
+    assert ands, "no level-1 partial products found"
+    m = T.MultiContext(keyset.bk, keyset.ksk, slots)
+    try:
+        y, dt, extra, (wires, in_a, in_b) = matvec.run_rows_multi(
+            T, m, keyset, C, a_w, x_w, y_w, A, xv, nbits, rng, extra_out=[w for w, _, _ in ands])
+    finally:
+        m.close()
+    assert np.array_equal(y, (A.astype(object) @ xv.astype(object)).astype(np.int64))
+    pos = {w: k for k, w in enumerate(wires)}
+    half = T.shard_range(R, 1, len(slots))[0]
+    rows = np.unique([0, half - 1, half, R - 1])
+    for w, i0, i1 in ands:
+        o_a, o_b = okey.gate_batch("AND", in_a[pos[i0]][rows], in_b[pos[i0]][rows], in_a[pos[i1]][rows],
+                                   in_b[pos[i1]][rows])
+        assert np.array_equal(extra[w][0][rows], o_a) and np.array_equal(extra[w][1][rows], o_b), w
+    print(f"64x64 16-bit matvec, all 64 rows over {len(slots)} device slots: {dt:.2f} s")
+
+
 def test_circuit_rows_torus32_vs_oracle(ctx, okey, keyset, rng):
     """k_blind_rotate_v6_rows + the circuit key switch: each bootstrapped row's output equals
     the oracle's bootstrap + key switch of the same linear combination, word for word, for

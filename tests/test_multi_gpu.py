@@ -78,6 +78,101 @@ def test_tfhe_gpu_init_and_boots_batch(ctx, keyset, rng):
     assert np.array_equal(keyset.decrypt(*after), x & (1 - y))
 
 
+def _slots():
+    """device slots for a multi-context: every visible GPU, or two contexts on device 0"""
+    n = _torch().cuda.device_count()
+    return list(range(n)) if n > 1 else [0, 0]
+
+
+def test_multi_gate_batch_dev_resident_shards(ctx, okey, keyset, rng):
+    """tfhe_amd_multi_gate_batch_dev: each slot's shard already in its device's HBM (no PCIe in the
+    loop), enqueued on every slot and synced; the shards equal one context's evaluation of the
+    whole batch word for word (NAND, ragged 3 + 2 split, and MUX), the oracle on the seams."""
+    torch = _torch()
+    slots = _slots()
+    m = T.MultiContext(keyset.bk, keyset.ksk, slots)
+    try:
+        for gate, B in (("NAND", 261), ("MUX", 67)):
+            bits = [rng.integers(0, 2, B) for _ in range(3 if gate == "MUX" else 2)]
+            host = [v for b in bits for v in keyset.encrypt(b, rng)]
+            want = ctx.gate_host(gate, *host)
+            shards, outs = [], []
+            for i, d in enumerate(slots):
+                lo, hi = T.shard_range(B, i, len(slots))
+                dev = [torch.from_numpy(np.ascontiguousarray(v[lo:hi])).to(f"cuda:{d}") for v in host]
+                r_a = torch.empty((hi - lo, 500), dtype=torch.int32, device=f"cuda:{d}")
+                r_b = torch.empty(hi - lo, dtype=torch.int32, device=f"cuda:{d}")
+                shards.append([r_a, r_b] + dev)
+                outs.append((lo, hi, r_a, r_b))
+            m.gate_dev(gate, shards)
+            m.sync()
+            got_a = np.concatenate([o[2].cpu().numpy() for o in outs])
+            got_b = np.concatenate([o[3].cpu().numpy() for o in outs])
+            assert np.array_equal(got_a, want[0]) and np.array_equal(got_b, want[1]), gate
+            seam = np.unique([0, outs[0][1] - 1, outs[0][1], B - 1])
+            o = okey.gate_batch(gate, *(v[seam] for v in host))
+            assert np.array_equal(got_a[seam], o[0]) and np.array_equal(got_b[seam], o[1]), gate
+    finally:
+        m.close()
+
+
+def _small_circuit():
+    C = T.Circuit()
+    a, b = C.inputs(8), C.inputs(8)
+    s, co = C.add(a, b)
+    gt = C.compare(a, b, "GT")
+    mn = C.minmax(a, b)
+    return C, a, b, s + [co, gt] + mn
+
+
+def test_multi_circuit_host_and_dev_equal_one_context(ctx, keyset, rng):
+    """tfhe_amd_multi_circuit_run_host / _run_dev: one circuit's instances sharded over the slots
+    (here 37 instances of 8-bit add + compare + min), each slot in its own HBM wire arrays; the
+    output wires equal one context's run of all 37 instances word for word, and decrypt to the
+    integer results."""
+    torch = _torch()
+    slots = _slots()
+    C, a, b, outs = _small_circuit()
+    B = 37
+    x, y = rng.integers(0, 256, B), rng.integers(0, 256, B)
+    x[0], y[0] = 255, 255
+    ins = a + b
+    planes = T.bits_of(x, 8) + T.bits_of(y, 8)
+    enc = [keyset.encrypt(p, rng) for p in planes]
+    in_a = np.stack([e[0] for e in enc]); in_b = np.stack([e[1] for e in enc])
+    n_w = C.info()["wires"]
+    # one context, all instances
+    wa = torch.zeros((n_w, B, 500), dtype=torch.int32, device="cuda")
+    wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+    wa[ins] = torch.from_numpy(in_a).cuda(); wb[ins] = torch.from_numpy(in_b).cuda()
+    C.run_dev(ctx, B, wa, wb)
+    torch.cuda.synchronize()
+    one_a, one_b = wa[outs].cpu().numpy(), wb[outs].cpu().numpy()
+    m = T.MultiContext(keyset.bk, keyset.ksk, slots)
+    try:
+        got_a, got_b = m.circuit_host(C, B, ins, in_a, in_b, outs)
+        assert np.array_equal(got_a, one_a) and np.array_equal(got_b, one_b)
+        shards = []
+        for i, d in enumerate(slots):
+            lo, hi = T.shard_range(B, i, len(slots))
+            sa = torch.zeros((n_w, hi - lo, 500), dtype=torch.int32, device=f"cuda:{d}")
+            sb = torch.zeros((n_w, hi - lo), dtype=torch.int32, device=f"cuda:{d}")
+            sa[ins] = torch.from_numpy(np.ascontiguousarray(in_a[:, lo:hi])).to(sa.device)
+            sb[ins] = torch.from_numpy(np.ascontiguousarray(in_b[:, lo:hi])).to(sb.device)
+            shards.append((sa, sb))
+        m.circuit_dev(C, shards)
+        m.sync()
+        dev_a = np.concatenate([sh[0][outs].cpu().numpy() for sh in shards], axis=1)
+        dev_b = np.concatenate([sh[1][outs].cpu().numpy() for sh in shards], axis=1)
+        assert np.array_equal(dev_a, one_a) and np.array_equal(dev_b, one_b)
+    finally:
+        m.close()
+    dec = [keyset.decrypt(got_a[k], got_b[k]) for k in range(len(outs))]
+    assert np.array_equal(T.int_of(dec[:9]), x + y)
+    assert np.array_equal(dec[9], (x > y).astype(np.int64))
+    assert np.array_equal(T.int_of(dec[10:]), np.minimum(x, y))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
