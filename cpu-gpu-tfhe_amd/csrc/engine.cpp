@@ -110,10 +110,12 @@ int br_version() {
     return v;
 }
 
-// high word of the rounding distance at which the exact kernel recomputes a ciphertext: 1/4
-// (0x3FD00000) by default; tfhe_amd_set_guard_threshold changes it (tests force the fallback with
-// 0; values >= 1/2 can never trigger, the distance being <= 1/2)
-static std::atomic<uint32_t> g_guard_hi{0x3FD00000u};
+// high word of the rounding distance at which the exact kernel recomputes a ciphertext: 1/8
+// (0x3FC00000) by default — 1.6x the largest distance real keys show (0.06-0.08), so that an
+// error can only escape by reaching 7/8 at a coefficient while every other rounding of the
+// ciphertext's 500 steps stays below 1/8; tfhe_amd_set_guard_threshold changes
+// it (tests force the fallback with 0; values >= 1/2 can never trigger, the distance being <= 1/2)
+static std::atomic<uint32_t> g_guard_hi{0x3FC00000u};
 uint32_t guard_threshold_hi() { return g_guard_hi.load(std::memory_order_relaxed); }
 
 // the default fp64 kernel, then the exact kernel in guard mode over the flags it wrote

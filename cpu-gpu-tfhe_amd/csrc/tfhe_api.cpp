@@ -524,6 +524,7 @@ struct Tier1Req {
     const LweSample *a, *b, *c;
     bool done = false;
     int rc = TFHE_AMD_OK;
+    std::vector<int32_t> u;   // its key-switch input: the caller derives current_variance from it
 };
 
 // Coalescing queue of the Tier-1 gates of one key ("per-thread streams or a
@@ -531,16 +532,18 @@ struct Tier1Req {
 // (Cipher.cpp:83-120, cloud.cpp:389-395); one B = 1 launch per call would occupy 2 waves of one
 // CU each, and a process has only 4 hardware queues.  Here a call enqueues its gate; whichever
 // waiting thread finds no batch running becomes the leader, takes every pending gate (grouped by
-// gate kind) and runs them as one batch per kind on its own lane, while the gates that arrive
-// meanwhile queue up for the next batch (group commit).  A lone thread is its own leader at once:
-// its B = 1 latency is the plain path's.  Once concurrency has been seen (the last batch held
-// more than one gate) the leader waits at most `window` for as many gates as that batch held.
+// gate kind) and runs them as one batch per kind on the queue's lane, while the gates that arrive
+// meanwhile queue up for the next batch (group commit).  Before it takes them the leader waits
+// until every thread inside a gate call has enqueued (threads whose gate just completed either
+// come back with their next gate or leave), at most `window` (TFHE_AMD_TIER1_WINDOW_US): so an
+// OpenMP team's gates of one iteration go out as one batch.  A lone thread is its own leader at
+// once: its B = 1 latency is the plain path's.
 struct Coalescer {
     std::mutex mu;
     std::condition_variable done_cv, arrive_cv;
     std::vector<Tier1Req *> pending;
+    int inside = 0;      // threads inside a Tier-1 gate call on this key
     bool busy = false;
-    size_t last_batch = 1;
     long long batches = 0, gates = 0, largest = 0;
 };
 
@@ -551,6 +554,7 @@ struct KeyEntry {
     std::vector<TfheAmdContext *> lanes;
     std::mutex mu;
     Coalescer q;
+    TfheAmdContext *qlane = nullptr;   // the coalescing queue's lane (used by one leader at a time)
 };
 static std::mutex g_reg_mu;
 static std::unordered_map<const void *, std::shared_ptr<KeyEntry>> g_reg;   // bkFFT or KSK -> entry
@@ -601,6 +605,8 @@ static void forget_device_keys(const void *k1, const void *k2) {
         std::lock_guard<std::mutex> lk(e->mu);
         for (auto *l : e->lanes) tfhe_amd_context_destroy(l);
         e->lanes.clear();
+        if (e->qlane) tfhe_amd_context_destroy(e->qlane);
+        e->qlane = nullptr;
         tfhe_amd_context_destroy(e->primary);
         e->primary = nullptr;
     }
@@ -754,7 +760,7 @@ EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const Lwe
 // ------------------------------------------------------------------ gates
 
 // TFHE_AMD_TIER1_COALESCE=0: every thread runs its own B = 1 batches on its own lane (no queue);
-// TFHE_AMD_TIER1_WINDOW_US: the leader's wait for stragglers (default 50 us)
+// TFHE_AMD_TIER1_WINDOW_US: the leader's longest wait for the threads inside a call (default 200 us)
 static bool coalesce_enabled() {
     static const bool on = [] {
         const char *e = getenv("TFHE_AMD_TIER1_COALESCE");
@@ -765,15 +771,15 @@ static bool coalesce_enabled() {
 static int coalesce_window_us() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_TIER1_WINDOW_US");
-        return e ? std::max(0, atoi(e)) : 50;
+        return e ? std::max(0, atoi(e)) : 200;
     }();
     return v;
 }
 
 // Runs one batch of queued gates on lane l: per gate kind one host batch (inputs staged before
-// anything is written, so a result may alias any input of its own call), then each output's
-// current_variance from its key-switch input, as the single-gate path.
-static void run_tier1_batch(TfheAmdContext *l, const LweKeySwitchKey *ks, const std::vector<Tier1Req *> &batch) {
+// anything is written, so a result may alias any input of its own call); each request gets its
+// key-switch input back, from which its caller sums current_variance as the single-gate path.
+static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
     std::vector<Tier1Req *> group;
     std::vector<int32_t> buf, u;
     std::vector<bool> taken(batch.size(), false);
@@ -814,7 +820,9 @@ static void run_tier1_batch(TfheAmdContext *l, const LweKeySwitchKey *ks, const 
                 Tier1Req *q = group[s0 + i];
                 memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
                 q->r->b = rb[s0 + i];
-                q->r->current_variance = ks_variance(ks, u.data() + (size_t)i * kN);
+                // current_variance is summed by each caller after the batch (in parallel, off the
+                // queue's critical path): 8 192 table reads per gate
+                q->u.assign(u.begin() + (size_t)i * kN, u.begin() + (size_t)(i + 1) * kN);
             }
         }
     }
@@ -822,8 +830,8 @@ static void run_tier1_batch(TfheAmdContext *l, const LweKeySwitchKey *ks, const 
 
 static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b, const LweSample *c,
                   const TFheGateBootstrappingCloudKeySet *bk) {
-    TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
     if (!coalesce_enabled()) {
+        TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
         check(tfhe_amd_gate_batch_host(l, gate, 1, r->a, &r->b, a->a, &a->b, b->a, &b->b, c ? c->a : nullptr,
                                        c ? &c->b : nullptr),
               "gate");
@@ -836,6 +844,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     Coalescer &q = e->q;
     Tier1Req req{gate, r, a, b, c};
     std::unique_lock<std::mutex> lk(q.mu);
+    q.inside += 1;
     q.pending.push_back(&req);
     q.arrive_cv.notify_one();
     while (!req.done) {
@@ -844,26 +853,35 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
             continue;
         }
         q.busy = true;   // this thread leads the next batch
-        if (q.last_batch > 1 && q.pending.size() < q.last_batch && coalesce_window_us() > 0) {
-            const size_t want = q.last_batch;
+        if ((int)q.pending.size() < q.inside && coalesce_window_us() > 0)
             q.arrive_cv.wait_for(lk, std::chrono::microseconds(coalesce_window_us()),
-                                 [&] { return q.pending.size() >= want; });
-        }
+                                 [&] { return (int)q.pending.size() >= q.inside; });
         std::vector<Tier1Req *> batch;
         batch.swap(q.pending);
         lk.unlock();
-        run_tier1_batch(l, bk->bkFFT->ks, batch);
+        // the queue's own lane (stream + scratch), not the leader thread's: a thread that only
+        // ever enqueues needs no lane, and leaders change from batch to batch
+        TfheAmdContext *l;
+        {
+            std::lock_guard<std::mutex> lg(e->mu);
+            if (!e->qlane) e->qlane = tfhe_amd_context_lane(e->primary);
+            l = e->qlane;
+        }
+        if (!l) die_dramatically("tfhe_amd: cannot create the Tier-1 queue's GPU lane");
+        run_tier1_batch(l, batch);
         lk.lock();
         for (Tier1Req *x : batch) x->done = true;
-        q.last_batch = batch.size();
         q.batches += 1;
         q.gates += (long long)batch.size();
         q.largest = std::max(q.largest, (long long)batch.size());
         q.busy = false;
         q.done_cv.notify_all();
     }
+    q.inside -= 1;
+    q.arrive_cv.notify_one();   // a leader may be waiting for this thread
     lk.unlock();
     check(req.rc, "gate");
+    r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
 }
 
 EXPORT int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches,

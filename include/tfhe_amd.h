@@ -186,11 +186,12 @@ int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const 
 int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
 
 /* Concurrent Tier-1 gate calls on one key are coalesced: a calling thread enqueues its gate; the
- * first waiting thread that finds no batch running takes every pending gate and runs them as one
- * batch per gate kind on its lane, while later calls queue for the next batch (a lone thread runs
- * its gate at once, B = 1).  Results, aliasing and current_variance are as for a lone call.
- * env TFHE_AMD_TIER1_COALESCE=0 disables the queue (per-thread B = 1 launches);
- * TFHE_AMD_TIER1_WINDOW_US (default 50) bounds a leader's wait for stragglers.
+ * first waiting thread that finds no batch running waits until every thread inside a gate call
+ * has enqueued (at most TFHE_AMD_TIER1_WINDOW_US, default 200 us), takes every pending gate and
+ * runs them as one batch per gate kind on the queue's lane, while later calls queue for the next
+ * batch (a lone thread runs its gate at once, B = 1).  Results, aliasing and current_variance are
+ * as for a lone call.  env TFHE_AMD_TIER1_COALESCE=0 disables the queue (per-thread lanes, B = 1
+ * launches).
  * queue_stats: batches run, gates they held, the largest batch (reset = 1 zeroes them). */
 int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches, long long *gates,
                                long long *largest, int reset);
@@ -224,10 +225,13 @@ int tfhe_amd_select_kernel(int br_version);
 int tfhe_amd_last_kernels(TfheAmdContext *ctx, char *buf, int cap);
 
 /* Exactness guard of the default fp64 FFT blind rotation: every launch
- * measures, per ciphertext, the largest distance |c - rint(c)| of any rounded external-product
- * coefficient over its 500 steps; a ciphertext at or above the threshold (default 1/4; the
- * result is exact while the FFT error stays below 1/2) is recomputed by the exact 2-prime NTT
- * kernel in the same stream before its key switch.  guard_stats reads (and optionally resets)
+ * measures, per ciphertext, the largest distance |c - rint(c)| of every rounded external-product
+ * coefficient over its 500 steps, and the range |c| < 2^51 of the rounding shifter; a ciphertext
+ * at or above the threshold (default 1/8), or out of range, is recomputed by the exact 2-prime
+ * NTT kernel in the same stream before its key switch.  The rule is statistical, not a proof: a
+ * wrong coefficient needs an FFT error >= 1/2, and one that shows a distance < 1/8 needs >= 7/8
+ * while all ~10^6 other roundings of that ciphertext stay below 1/8 (real keys: largest
+ * distance 0.06-0.08, FFT errors of one step spread over all its coefficients).  guard_stats reads (and optionally resets)
  * the context's largest measured distance and its count of recomputed ciphertexts (it
  * synchronizes the device).  set_guard_threshold is process-wide (0 recomputes everything:
  * tests). */

@@ -19,4 +19,7 @@ LINK="-L$LIBDIR -ltfhe_amd -Wl,-rpath,$LIBDIR"
 g++ -std=c++11 -O2 $INC "$REF/main.cpp" -o "$OUT/main" $LINK -lgomp
 g++ -std=c++11 -O2 -fopenmp $INC "$REF/cloud.cpp" "$REF/Cipher.cpp" -o "$OUT/cloud" $LINK
 g++ -std=c++11 -O2 -fopenmp $INC "$REPO/tests/callers/cipher_ops.cpp" "$REF/Cipher.cpp" -o "$OUT/cipher_ops" $LINK
-echo "built $OUT/{main,cloud,cipher_ops}"
+# the same with Cipher.cpp's own OpenMP loops switched on (its `#define PARALLEL`, left commented
+# out at Cipher.cpp:13, given on the command line: the source stays unchanged)
+g++ -std=c++11 -O2 -fopenmp -DPARALLEL $INC "$REPO/tests/callers/cipher_ops.cpp" "$REF/Cipher.cpp" -o "$OUT/cipher_ops_par" $LINK
+echo "built $OUT/{main,cloud,cipher_ops,cipher_ops_par}"

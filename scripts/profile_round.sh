@@ -9,7 +9,9 @@ BATCH=${2:-1024}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --batch $BATCH --no-cpu-baseline --no-clock --no-ceiling --extra-batches none --strong-batch 0"
+# the bench's own warm-up (10) and step count (20), so that the profiler's average of the blind
+# rotation is over settled launches like the line's kernel_ms (scripts/trace_mean.py compares them)
+BENCH="$R/bench.py --steps 20 --warmup 10 --batch $BATCH --no-cpu-baseline --no-clock --no-ceiling --extra-batches none --strong-batch 0 --parity-samples 0"
 run() {   # name, extra rocprofv3 args...
   local name=$1; shift
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH > "$OUT/$name.log" 2>&1
@@ -19,6 +21,8 @@ run() {   # name, extra rocprofv3 args...
   return 0
 }
 run trace --kernel-trace --stats
+python3 "$R/scripts/trace_mean.py" "$(find "$OUT/trace" -name '*kernel_trace.csv' | head -n 1)" \
+    "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -n 1)" "$OUT/trace.log" 20 > "$OUT/trace_mean.json" 2>&1 || true
 run fetch --kernel-trace --pmc FETCH_SIZE
 run write --kernel-trace --pmc WRITE_SIZE
 run sq --kernel-trace --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY

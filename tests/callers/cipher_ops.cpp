@@ -8,7 +8,8 @@
 //   a * b (operator*, shift-and-add; on the low 8 bits), minimum(a, b), a == b, a > b.
 // `cipher_ops add32 A B`: BASELINE config 3 through the unchanged Cipher::operator+
 // (Cipher.cpp:348-392, 5 gates per bit) on 32-bit operands encrypted here with
-// bootsSymEncrypt under secret.key; prints {"a", "b", "sum", "seconds"}.
+// bootsSymEncrypt under secret.key; prints {"a", "b", "sum", "seconds", "first_gate_seconds"}.
+// `cipher_ops mul16 A B [threads]`: Cipher::operator* on 16-bit operands (see mul16 below).
 // Integration tests only (tests/test_io.py::test_reference_callers_gpu,
 // tests/test_configs_gpu.py::test_config3_cipher_operator_plus_32bit).
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include <string>
 
 #include "Cipher.h"
+#include "tfhe_amd.h"
 
 static long decode(const Cipher &c, const TFheGateBootstrappingSecretKeySet *key) {
     long v = 0;
@@ -34,11 +36,51 @@ static int add32(const TFheGateBootstrappingSecretKeySet *key, long av, long bv)
         bootsSymEncrypt(&y[i], (int)((bv >> i) & 1), key);
     }
     Cipher a(bits, x), b(bits, y);
+    // the first gate call of a process builds the key's device context (HIP initialisation, code
+    // objects, key upload + conversion on the GPU, this thread's lane): timed on its own, then the
+    // addition itself — what the reference times too, its keys being loaded before
+    LweSample *w = new_gate_bootstrapping_ciphertext_array(1, params);
     double t0 = omp_get_wtime();
-    Cipher sum = a + b;
+    bootsAND(w, &x[0], &y[0], Cipher::bk);
     double t1 = omp_get_wtime();
-    printf("{\"a\": %ld, \"b\": %ld, \"sum\": %ld, \"seconds\": %.4f}\n", decode(a, key), decode(b, key),
-           decode(sum, key), t1 - t0);
+    Cipher sum = a + b;
+    double t2 = omp_get_wtime();
+    printf("{\"a\": %ld, \"b\": %ld, \"sum\": %ld, \"seconds\": %.4f, \"first_gate_seconds\": %.4f, "
+           "\"gates\": 160, \"ms_per_gate\": %.3f}\n", decode(a, key), decode(b, key), decode(sum, key), t2 - t1,
+           t1 - t0, 1e3 * (t2 - t1) / 160);
+    delete_gate_bootstrapping_ciphertext_array(1, w);
+    return 0;
+}
+
+// `cipher_ops mul16 A B [threads]`: the unchanged Cipher::operator* (Cipher.cpp:83-112) on 16-bit
+// operands -> 32-bit product.  Built twice (oracle/build_callers.sh): cipher_ops runs the loop
+// sequentially (Cipher.cpp leaves PARALLEL undefined), cipher_ops_par compiles Cipher.cpp with
+// -DPARALLEL, so the partial products run on an OpenMP team of Cipher::nThreads = `threads`
+// threads with the Cipher-sum reduction; their concurrent single-gate calls are what the
+// library's Tier-1 coalescing queue batches.
+static int mul16(const TFheGateBootstrappingSecretKeySet *key, long av, long bv, int threads) {
+    const TFheGateBootstrappingParameterSet *params = Cipher::bk->params;
+    const int bits = 16;
+    LweSample *x = new_gate_bootstrapping_ciphertext_array(bits, params);
+    LweSample *y = new_gate_bootstrapping_ciphertext_array(bits, params);
+    for (int i = 0; i < bits; i++) {
+        bootsSymEncrypt(&x[i], (int)((av >> i) & 1), key);
+        bootsSymEncrypt(&y[i], (int)((bv >> i) & 1), key);
+    }
+    Cipher a(bits, x), b(bits, y);
+    Cipher::nThreads = threads;
+    LweSample *w = new_gate_bootstrapping_ciphertext_array(1, params);
+    bootsAND(w, &x[0], &y[0], Cipher::bk);   // device context built outside the timed region
+    long long nb0 = 0, ng0 = 0, big = 0;
+    tfhe_amd_tier1_queue_stats(Cipher::bk, nullptr, nullptr, nullptr, 1);
+    double t0 = omp_get_wtime();
+    Cipher prod = a * b;
+    double t1 = omp_get_wtime();
+    tfhe_amd_tier1_queue_stats(Cipher::bk, &nb0, &ng0, &big, 0);
+    printf("{\"a\": %ld, \"b\": %ld, \"prod\": %ld, \"seconds\": %.4f, \"threads\": %d, \"gates\": %lld, "
+           "\"batches\": %lld, \"largest_batch\": %lld}\n", decode(a, key), decode(b, key), decode(prod, key),
+           t1 - t0, threads, ng0, nb0, big);
+    delete_gate_bootstrapping_ciphertext_array(1, w);
     return 0;
 }
 
@@ -48,6 +90,8 @@ int main(int argc, char **argv) {
     TFheGateBootstrappingSecretKeySet *key = new_tfheGateBootstrappingSecretKeySet_fromFile(f);
     fclose(f);
     if (argc == 4 && std::string(argv[1]) == "add32") return add32(key, atol(argv[2]), atol(argv[3]));
+    if (argc >= 4 && std::string(argv[1]) == "mul16")
+        return mul16(key, atol(argv[2]), atol(argv[3]), argc > 4 ? atoi(argv[4]) : 4);
     const TFheGateBootstrappingParameterSet *params = Cipher::bk->params;
     const int bits = 16;
     LweSample *x = new_gate_bootstrapping_ciphertext_array(bits, params);

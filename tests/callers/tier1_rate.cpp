@@ -1,0 +1,103 @@
+// tier1_rate.cpp — Tier-1 gate throughput from OpenMP teams (the reference's
+// callers enter single gates from `#pragma omp parallel for` loops, Cipher.cpp:83-120,
+// cloud.cpp:389-395).  Built against include/ + libtfhe_amd only (tests/callers/Makefile).
+//
+// A pool of P encrypted input pairs; every gate is bootsNAND(pool[i]) or, for odd i in the
+// threaded runs, bootsNAND written in place over a copy of its first input (the result aliases
+// an input, Cipher.cpp:306).  For each thread count T in argv (default 1 8 64) the team runs
+// `per_thread` gates per thread (schedule static), timed; every output must equal the sequential
+// result of the same gate word for word, and decrypt to the truth table.  The library's queue
+// statistics (tfhe_amd_tier1_queue_stats) say how the calls were batched.  Run it with
+// TFHE_AMD_TIER1_COALESCE=0 for the per-thread-lane path.
+// Prints one JSON line; exit status 0 only when everything matched.
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <omp.h>
+#include "tfhe/tfhe.h"
+#include "tfhe_amd.h"
+
+static bool same(const LweSample *x, const LweSample *y, int n) {
+    return x->b == y->b && memcmp(x->a, y->a, sizeof(Torus32) * n) == 0;
+}
+
+int main(int argc, char **argv) {
+    const int per_thread = argc > 1 ? atoi(argv[1]) : 8;
+    std::vector<int> teams;
+    for (int i = 2; i < argc; ++i) teams.push_back(atoi(argv[i]));
+    if (teams.empty()) teams = {1, 8, 64};
+    int maxT = 1;
+    for (int t : teams) maxT = t > maxT ? t : maxT;
+    const int P = maxT * per_thread;
+
+    uint32_t seed[] = {314, 1592, 657};
+    tfhe_random_generator_setSeed(seed, 3);
+    TFheGateBootstrappingParameterSet *params = new_default_gate_bootstrapping_parameters(110);
+    TFheGateBootstrappingSecretKeySet *key = new_random_gate_bootstrapping_secret_keyset(params);
+    const TFheGateBootstrappingCloudKeySet *bk = &key->cloud;
+    const LweParams *lp = params->in_out_params;
+    const int dim = lp->n;
+
+    std::vector<int> xa(P), xb(P);
+    uint32_t s = 2024u;
+    auto bit = [&]() { s = s * 1664525u + 1013904223u; return (int)(s >> 31); };
+    LweSample *a = new_gate_bootstrapping_ciphertext_array(P, params);
+    LweSample *b = new_gate_bootstrapping_ciphertext_array(P, params);
+    for (int i = 0; i < P; i++) {
+        xa[i] = bit(); xb[i] = bit();
+        bootsSymEncrypt(&a[i], xa[i], key);
+        bootsSymEncrypt(&b[i], xb[i], key);
+    }
+    LweSample *seq = new_gate_bootstrapping_ciphertext_array(P, params);
+    LweSample *out = new_gate_bootstrapping_ciphertext_array(P, params);
+    // warm-up (device context, key upload and conversion, lane) outside every timed region
+    bootsNAND(&out[0], &a[0], &b[0], bk);
+    double t0 = omp_get_wtime();
+    for (int i = 0; i < P; i++) bootsNAND(&seq[i], &a[i], &b[i], bk);
+    const double seq_s = omp_get_wtime() - t0;
+    int truth_errors = 0;
+    for (int i = 0; i < P; i++) truth_errors += bootsSymDecrypt(&seq[i], key) != !(xa[i] & xb[i]);
+
+    std::string runs;
+    int mismatches = 0;
+    for (int T : teams) {
+        const int n = T * per_thread;
+        // untimed warm-up of the team (OpenMP threads created; per-thread lanes when the queue is off)
+#pragma omp parallel for num_threads(T) schedule(static)
+        for (int t = 0; t < T; t++) bootsNAND(&out[t], &a[t], &b[t], bk);
+        for (int i = 0; i < n; i++) lweCopy(&out[i], &a[i], lp);
+        tfhe_amd_tier1_queue_stats(bk, nullptr, nullptr, nullptr, 1);
+        t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(T) schedule(static)
+        for (int i = 0; i < n; i++) {
+            if (i & 1) bootsNAND(&out[i], &out[i], &b[i], bk);   // in place: result aliases input a
+            else bootsNAND(&out[i], &a[i], &b[i], bk);
+        }
+        const double dt = omp_get_wtime() - t0;
+        long long nb = 0, ng = 0, big = 0;
+        tfhe_amd_tier1_queue_stats(bk, &nb, &ng, &big, 1);
+        int bad = 0;
+        for (int i = 0; i < n; i++) bad += !same(&out[i], &seq[i], dim);
+        mismatches += bad;
+        char line[256];
+        snprintf(line, sizeof line,
+                 "%s{\"threads\": %d, \"gates\": %d, \"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, "
+                 "\"batches\": %lld, \"mean_batch\": %.2f, \"largest_batch\": %lld}",
+                 runs.empty() ? "" : ", ", T, n, dt, n / dt, bad, nb, nb ? (double)ng / nb : 0.0, big);
+        runs += line;
+    }
+    const char *co = getenv("TFHE_AMD_TIER1_COALESCE");
+    printf("{\"coalesce\": %s, \"pool\": %d, \"sequential_gates_per_s\": %.1f, \"truth_errors\": %d, "
+           "\"mismatches\": %d, \"runs\": [%s]}\n",
+           co && co[0] == '0' ? "false" : "true", P, P / seq_s, truth_errors, mismatches, runs.c_str());
+    delete_gate_bootstrapping_ciphertext_array(P, out);
+    delete_gate_bootstrapping_ciphertext_array(P, seq);
+    delete_gate_bootstrapping_ciphertext_array(P, b);
+    delete_gate_bootstrapping_ciphertext_array(P, a);
+    delete_gate_bootstrapping_secret_keyset(key);
+    delete_gate_bootstrapping_parameters(params);
+    return truth_errors || mismatches ? 1 : 0;
+}

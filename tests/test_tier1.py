@@ -37,6 +37,34 @@ def test_tier1_threads_and_aliasing_gpu():
     assert out["short_thread_errors"] == 0 and out["lanes_after_short_threads"] == out["lanes_before"], out
 
 
+def _rate_run(env_extra, args):
+    exe = os.path.join(CALLERS, "_bin", "tier1_rate")
+    assert os.access(exe, os.X_OK), "tests/callers/_bin/tier1_rate missing: run __graft_entry__.build()"
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([exe] + [str(a) for a in args], capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (r.returncode, r.stderr[-2000:])
+    out = json.loads(lines[-1])
+    assert r.returncode == 0, (out, r.stderr[-2000:])
+    return out
+
+
+@pytest.mark.gpu
+def test_tier1_coalescing_queue_rate():
+    """Concurrent single-gate calls (OpenMP teams of 1, 8 and 64 threads, half of them in place)
+    through the coalescing queue: every output equals the sequential result word for word, and 64
+    threads reach >= 20x the one-thread gate rate; the per-thread-lane path
+    (TFHE_AMD_TIER1_COALESCE=0) is measured beside it."""
+    q = _rate_run({}, [16, 1, 8, 64])
+    lanes = _rate_run({"TFHE_AMD_TIER1_COALESCE": "0"}, [16, 1, 8, 64])
+    print(json.dumps({"queue": q, "per_thread_lanes": lanes}))
+    for out in (q, lanes):
+        assert out["truth_errors"] == 0 and out["mismatches"] == 0, out
+    rate = {r["threads"]: r["gates_per_s"] for r in q["runs"]}
+    assert rate[64] >= 20 * rate[1], q
+    assert max(r["largest_batch"] for r in q["runs"]) > 1, q
+
+
 @pytest.mark.gpu
 def test_tier1_single_gate_latency():
     """Sequential single-gate calls through the C API (what an unchanged Cipher.cpp caller sees):
