@@ -956,7 +956,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
 #endif
         } else if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
-            trace_kernel("k_blind_rotate_v6p(paired,reg-rotation)");
+            trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
             hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
                                v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
         } else {

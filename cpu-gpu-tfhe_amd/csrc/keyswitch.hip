@@ -693,8 +693,8 @@ static void launch_ks5(const uint4 *w5, int count, const P &io, hipStream_t s) {
     const int split = ks5_split(mtiles);
     if (split > 1) hipLaunchKernelGGL(k_keyswitch_small_init<P>, dim3(count), dim3(512), 0, s, io);
     const dim3 grid(mtiles * kKs5Nb * split);
-    trace_kernel(split == 8 ? "k_keyswitch_v5(int8-mfma,split8)" : split == 4 ? "k_keyswitch_v5(int8-mfma,split4)"
-                 : split == 2 ? "k_keyswitch_v5(int8-mfma,split2)" : "k_keyswitch_v5(int8-mfma)");
+    trace_kernel(split == 8 ? "k_keyswitch_v5(int8-mfma+split8)" : split == 4 ? "k_keyswitch_v5(int8-mfma+split4)"
+                 : split == 2 ? "k_keyswitch_v5(int8-mfma+split2)" : "k_keyswitch_v5(int8-mfma)");
     switch (split) {
     case 8: hipLaunchKernelGGL((k_keyswitch_v5<P, 8, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;
     case 4: hipLaunchKernelGGL((k_keyswitch_v5<P, 4, MS>), grid, dim3(kKs5Threads), 0, s, w5, io); break;

@@ -218,7 +218,7 @@ int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32
 int tfhe_amd_select_kernel(int br_version);
 
 /* The kernels (with the variant the launch geometry picked, e.g. "k_blind_rotate_v6(reg-rotation)",
- * "k_blind_rotate_v4(guard)", "k_keyswitch_v5(int8-mfma,split2)") that the context's last batch
+ * "k_blind_rotate_v4(guard)", "k_keyswitch_v5(int8-mfma+split2)") that the context's last batch
  * call enqueued, comma-separated in first-launch order, NUL-terminated into buf[cap].  Returns the
  * full length (which may exceed cap - 1).  For smoke / bench reports of which kernels produced
  * the checked outputs. */
