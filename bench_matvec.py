@@ -4,6 +4,8 @@ rows sharded over GPUs (cpu-gpu-tfhe_amd/matvec.py).  One process per GPU:
     python bench_matvec.py                                   # 1 GPU, all 64 rows
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench_matvec.py
     python bench_matvec.py --rank-of 0 --world-of 8          # rehearse one rank's 1/8 shard
+    python bench_matvec.py --multi 0,1,2,3,4,5,6,7           # ONE process, rows sharded over
+                                                             # device slots inside the library
 
 Timed region: every rank's whole circuit (all levels), bracketed by barrier + synchronize,
 max over ranks.  Each rank decrypts its rows and checks them against integer arithmetic
@@ -28,7 +30,11 @@ def main():
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--rank-of", type=int, default=0, help="single-process rehearsal: act as this rank")
     ap.add_argument("--world-of", type=int, default=1, help="single-process rehearsal: of this many ranks")
+    ap.add_argument("--multi", default="", help="one process: device slots of a MultiContext, e.g. 0,1 or "
+                    "'all' (tfhe_amd_multi_circuit_run_host shards the rows over them)")
     args = ap.parse_args()
+    if args.multi:
+        return main_multi(args)
     import torch
     import torch.distributed as dist
     import shard
@@ -74,6 +80,38 @@ def main():
     K.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_multi(args):
+    """All rows from one host process through tfhe_amd_multi_circuit_run_host (matvec.run_rows_multi):
+    the library shards the rows over the device slots (one worker thread + key replica each).
+    Timed: the whole call (staging in, every level on every device, outputs back)."""
+    import torch
+    import matvec
+    import tfhe_amd as T
+    slots = (list(range(torch.cuda.device_count())) if args.multi == "all"
+             else [int(d) for d in args.multi.split(",")])
+    K = T.SecretKeyset()
+    data_rng = np.random.default_rng(2024)
+    A = data_rng.integers(0, 2**args.nbits, (args.rows, args.cols))
+    x = data_rng.integers(0, 2**args.nbits, args.cols)
+    C, a_w, x_w, y_w = matvec.build(T, args.cols, args.nbits)
+    info = C.info()
+    m = T.MultiContext(K.bk, K.ksk, slots)
+    times, ok = [], True
+    for r in range(args.reps + 1):                       # the first run warms up (tables, scratch)
+        y, t, _, _ = matvec.run_rows_multi(T, m, K, C, a_w, x_w, y_w, A, x, args.nbits, np.random.default_rng(100 + r))
+        ok = ok and bool(np.array_equal(y, A @ x))
+        if r:
+            times.append(t)
+    m.close()
+    t = float(np.median(times))
+    print(json.dumps({"metric": f"encrypted {args.rows}x{args.cols} matrix-vector product ({args.nbits}-bit) wall time",
+                      "value": t, "unit": "s", "higher_is_better": False, "mode": "one process, multi-device",
+                      "slots": slots, "n_devices": len(set(slots)), "bootstraps_per_row": info["bootstraps"],
+                      "depth": info["depth"], "bootstraps_per_s": info["bootstraps"] * args.rows / t,
+                      "correct": ok, "engine": T.version(), "reps": args.reps}), flush=True)
+    K.close()
 
 
 if __name__ == "__main__":
