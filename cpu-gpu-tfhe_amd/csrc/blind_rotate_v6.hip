@@ -323,11 +323,29 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im); mx tracks the
     // rounding distance for the exactness guard
+#ifdef TFHE_AMD_V6_GUARD_HALF
+    // A/B experiment: measure the real parts on even steps and the imaginary parts on odd ones
+    // (every coefficient every other step; half the guard's VALU)
+    if (i & 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            acc[r] += (uint32_t)__double_as_longlong(Y[r].re + 0x1.8p52);
+            acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
+            acc[r + 8] += (uint32_t)__double_as_longlong(Y[r].im + 0x1.8p52);
+        }
+    }
+#else
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
         acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
     }
+#endif
     wave_sync();
     V6_STAMP(8);
 }
