@@ -187,7 +187,7 @@ struct TfheAmdContext {
     bool shared_key = false;   // lane: the key belongs to another context
     StreamFence fence;         // u_a / u_b reuse across caller streams
     // sliced host batches (gate_batch_host_sliced): copy streams and their events
-    hipStream_t copy_in = nullptr, copy_out = nullptr;
+    hipStream_t copy_in = nullptr;
     hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out[2] = {nullptr, nullptr};
     std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
 };
@@ -373,7 +373,6 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     for (hipEvent_t e : {c->ev_in, c->ev_done, c->ev_out[0], c->ev_out[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->copy_in) (void)hipStreamDestroy(c->copy_in);
-    if (c->copy_out) (void)hipStreamDestroy(c->copy_out);
     free_scratch(c);
     if (c->gstats) (void)hipFree(c->gstats);
     if (!c->shared_key) free_key(c->key);
@@ -645,43 +644,49 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
                                   const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
     if (!c->copy_in) {
         HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking));
         for (hipEvent_t *e : {&c->ev_in, &c->ev_done, &c->ev_out[0], &c->ev_out[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    const size_t A = (size_t)B * kn;
-    int32_t *h = c->h_io, *d = c->io, *hb = h + 4 * A, *db = d + 4 * A;
+    // Staging layout (pinned h_io and device io alike): slice s's inputs as ONE contiguous block
+    // at word 501 nin s0 — [a_0 | a_1 (| a_2) | b_0 | b_1 (| b_2)] — and its results at
+    // 3 * 501 B + 501 s0 — [res_a | res_b].  One copy per slice and direction: the input block is
+    // large enough for the copy engine (SDMA), which runs beside the blind rotation of the
+    // previous slice; the small per-array copies of the round-2 layout went to blit kernels that
+    // could not start while a blind rotation held every CU (rocprofv3 trace: 3.1-3.4 ms stalls),
+    // serialising the pipeline.  The result copy is a blit kernel too, so it is issued on the
+    // compute stream right behind its key switch, ahead of the next slice's blind rotation.
+    constexpr size_t R = kn + 1;
+    int32_t *h = c->h_io, *d = c->io;
+    const size_t out0 = 3 * R * (size_t)B;
     const int S = host_slice();
     const int nsl = (B + S - 1) / S;
     auto unstage = [&](int s) -> int {
         const int s0 = s * S, n = std::min(S, B - s0);
+        const int32_t *ho = h + out0 + R * (size_t)s0;
         HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
-        memcpy(res_a + (size_t)s0 * kn, h + 3 * A + (size_t)s0 * kn, (size_t)n * kn * 4);
-        memcpy(res_b + s0, hb + 3 * (size_t)B + s0, (size_t)n * 4);
+        memcpy(res_a + (size_t)s0 * kn, ho, (size_t)n * kn * 4);
+        memcpy(res_b + s0, ho + (size_t)n * kn, (size_t)n * 4);
         return TFHE_AMD_OK;
     };
     for (int s = 0; s < nsl; ++s) {
         const int s0 = s * S, n = std::min(S, B - s0);
-        const size_t o = (size_t)s0 * kn, na = (size_t)n * kn;
+        const size_t na = (size_t)n * kn, blk = R * (size_t)nin * s0;
+        int32_t *hi = h + blk, *di = d + blk;
         for (int k = 0; k < nin; ++k) {
-            int32_t *ha = h + k * A + o, *hbk = hb + (size_t)k * B + s0;
-            memcpy(ha, in_a[k] + o, na * 4);
-            memcpy(hbk, in_b[k] + s0, (size_t)n * 4);
-            HIPCHK(hipMemcpyAsync(d + k * A + o, ha, na * 4, hipMemcpyHostToDevice, c->copy_in));
-            HIPCHK(hipMemcpyAsync(db + (size_t)k * B + s0, hbk, (size_t)n * 4, hipMemcpyHostToDevice, c->copy_in));
+            memcpy(hi + k * na, in_a[k] + (size_t)s0 * kn, na * 4);
+            memcpy(hi + nin * na + (size_t)k * n, in_b[k] + s0, (size_t)n * 4);
         }
+        HIPCHK(hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in));
         HIPCHK(hipEventRecord(c->ev_in, c->copy_in));
         HIPCHK(hipStreamWaitEvent(c->stream, c->ev_in, 0));
-        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, d + 3 * A + o, db + 3 * (size_t)B + s0, d + o, db + s0,
-                                               d + A + o, db + B + s0, nin > 2 ? d + 2 * A + o : nullptr,
-                                               nin > 2 ? db + 2 * (size_t)B + s0 : nullptr, c->stream);
+        const int32_t *da = di, *db = di + nin * na;
+        int32_t *dout = d + out0 + R * (size_t)s0;
+        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, da, db, da + na, db + n,
+                                               nin > 2 ? da + 2 * na : nullptr, nin > 2 ? db + 2 * n : nullptr,
+                                               c->stream);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(c->ev_done, c->stream));
-        HIPCHK(hipStreamWaitEvent(c->copy_out, c->ev_done, 0));
-        HIPCHK(hipMemcpyAsync(h + 3 * A + o, d + 3 * A + o, na * 4, hipMemcpyDeviceToHost, c->copy_out));
-        HIPCHK(hipMemcpyAsync(hb + 3 * (size_t)B + s0, db + 3 * (size_t)B + s0, (size_t)n * 4,
-                              hipMemcpyDeviceToHost, c->copy_out));
-        HIPCHK(hipEventRecord(c->ev_out[s & 1], c->copy_out));
+        HIPCHK(hipMemcpyAsync(h + out0 + R * (size_t)s0, dout, R * (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(c->ev_out[s & 1], c->stream));
         if (s > 0) {
             const int r = unstage(s - 1);
             if (r) return r;
@@ -718,7 +723,6 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
             // against the next call's staging on c->stream: drain everything before returning
             if (c->copy_in) (void)hipStreamSynchronize(c->copy_in);
             (void)hipStreamSynchronize(c->stream);
-            if (c->copy_out) (void)hipStreamSynchronize(c->copy_out);
         }
         return rc;
     }
