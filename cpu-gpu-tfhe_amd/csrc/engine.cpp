@@ -186,9 +186,9 @@ struct TfheAmdContext {
     std::mutex mu;
     bool shared_key = false;   // lane: the key belongs to another context
     StreamFence fence;         // u_a / u_b reuse across caller streams
-    // sliced host batches (gate_batch_host_sliced): copy streams and their events
+    // sliced host batches (gate_batch_host_sliced): the input copy stream and the events
     hipStream_t copy_in = nullptr;
-    hipEvent_t ev_in = nullptr, ev_done = nullptr, ev_out[2] = {nullptr, nullptr};
+    hipEvent_t ev_in = nullptr, ev_out[2] = {nullptr, nullptr};
     std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
 };
 
@@ -370,7 +370,7 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : c->ks_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     c->fence.release();
-    for (hipEvent_t e : {c->ev_in, c->ev_done, c->ev_out[0], c->ev_out[1]})
+    for (hipEvent_t e : {c->ev_in, c->ev_out[0], c->ev_out[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->copy_in) (void)hipStreamDestroy(c->copy_in);
     free_scratch(c);
@@ -644,7 +644,7 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
                                   const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
     if (!c->copy_in) {
         HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
-        for (hipEvent_t *e : {&c->ev_in, &c->ev_done, &c->ev_out[0], &c->ev_out[1]})
+        for (hipEvent_t *e : {&c->ev_in, &c->ev_out[0], &c->ev_out[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     // Staging layout (pinned h_io and device io alike): slice s's inputs as ONE contiguous block
@@ -719,7 +719,7 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
         const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
         rc = gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);
         if (rc) {
-            // copies of earlier slices may still be in flight on the copy streams, not ordered
+            // copies of earlier slices may still be in flight on the copy stream, not ordered
             // against the next call's staging on c->stream: drain everything before returning
             if (c->copy_in) (void)hipStreamSynchronize(c->copy_in);
             (void)hipStreamSynchronize(c->stream);

@@ -80,7 +80,7 @@ struct StreamFence {
 // FFT error stays below 1/2.  Every wave tracks the largest rounding distance |c - rint(c)| it
 // sees over all 500 steps and stores its high word (monotone in the distance) in flags[2 slot + w];
 // an exact-NTT (v4) launch in guard mode then recomputes every ciphertext whose flag reaches the
-// threshold (1/4 by default) and exits at once for all others.  stats[0] counts the recomputed
+// threshold (1/8 by default) and exits at once for all others.  stats[0] counts the recomputed
 // ciphertexts, stats[1] holds the largest high word seen (tfhe_amd_guard_stats).
 struct Guard {
     uint32_t *flags = nullptr;

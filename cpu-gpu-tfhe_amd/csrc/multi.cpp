@@ -7,7 +7,7 @@
 // arithmetic as shard.py's shard_range), every device holds a full replica of the key (its own
 // TfheAmdContext: FFT- and NTT-domain bootstrapping keys + key-switching layouts, uploaded once),
 // and one persistent worker thread per device stages its shard, runs it (the single-device host
-// path: pinned staging, copy streams, one-round launches) and copies it back.  There is no
+// path: pinned staging, a copy stream, one-round launches) and copies it back.  There is no
 // collective: the shards are independent and land in disjoint rows of the caller's arrays.
 #include <hip/hip_runtime.h>
 

@@ -244,9 +244,9 @@ def test_mux_split_keyswitch(ctx, okey, keyset, rng):
 
 
 def test_host_batch_slices(ctx, okey, keyset, rng):
-    """Host-pointer batches above one round are pipelined in slices of 1024 over two copy
-    streams; a 3-input MUX batch of 2 100 (slices 1024 / 1024 / 52) decrypts right and matches
-    the oracle at every slice seam."""
+    """Host-pointer batches above one round are pipelined in slices of 1024 (one contiguous input
+    copy per slice on a copy stream, the result copy behind each key switch); a 3-input MUX batch
+    of 2 100 (slices 1024 / 1024 / 52) decrypts right and matches the oracle at every slice seam."""
     B = 2100
     s, x, y = (rng.integers(0, 2, B) for _ in range(3))
     (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
