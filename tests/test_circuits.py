@@ -320,3 +320,28 @@ def test_signed_division_gpu(ctx, keyset, rng):
     want = np.array([(-1 if (p < 0) != (d < 0) else 1) * (abs(int(p)) // abs(int(d))) for p, d in zip(xs, ys)])
     assert np.array_equal(_value(got, q), want % 2**n)
     print(f"8-bit signed division circuit: depth {C.info()['depth']}, {C.info()['bootstraps']} bootstraps")
+
+
+def test_circuit_oracle_evaluator_decrypts_like_plaintext(keyset, okey):
+    """The checker of tests/test_configs_gpu.py::test_circuits_every_wire_torus32_vs_oracle
+    (tests/circuit_oracle.py, exact oracle bootstraps node by node) decrypts, on every wire of a
+    small circuit with NOT / CONST / MUX / MAJ / XOR3 / lincomb nodes, to the circuit's plaintext
+    evaluation (CPU only)."""
+    import circuit_oracle
+    rng = np.random.default_rng(3)
+    C = T.Circuit()
+    a, b = C.inputs(3), C.inputs(3)
+    s, co = C.add(a, b)
+    mn = C.minmax(a, b)
+    na = C.gate("NOT", a[0])
+    one = C.gate("CONST", 1)
+    C.gate("MUX", na, one, b[1])
+    C.lincomb(1 << 29, 2, a[1], 1, b[2], 1, na)
+    B = 2
+    bits = {w: rng.integers(0, 2, B) for w in a + b}
+    enc = {w: keyset.encrypt(v, rng) for w, v in bits.items()}
+    W = circuit_oracle.eval_circuit(C, okey, enc, B, nthreads=8)
+    ref = C.eval_plain(bits)
+    for w in range(C.info()["wires"]):
+        dec = keyset.decrypt(*W[w])
+        assert np.array_equal(dec, np.broadcast_to(ref[w], dec.shape)), w   # CONST wires: a scalar

@@ -206,6 +206,54 @@ def test_config5_matvec_64x64_16bit_all_rows_multi_device(okey, keyset, rng):
     print(f"64x64 16-bit matvec, all 64 rows over {len(slots)} device slots: {dt:.2f} s")
 
 
+def _circuits_for_torus32():
+    """(name, circuit, {input wire: bit plane}) cases: BASELINE config 3 at its size (one 32-bit
+    ripple-carry addition), and config 4's multiplier, the comparison, min and division builders
+    at 8 / 6 bits so that the oracle checks every wire within seconds."""
+    r = np.random.default_rng(77)
+    B = 2
+    out = []
+    C = T.Circuit(); a, b = C.inputs(32), C.inputs(32); C.add(a, b)
+    x = np.array([0xFFFFFFFF, 0x89ABCDEF]); y = np.array([1, 0x76543211])
+    out.append(("config3 add32", C, {**_bits(a, x, 32), **_bits(b, y, 32)}, B))
+    for name, nb, build in (("mul8x8", 8, lambda C, a, b: C.mul(a, b)),
+                            ("signed a > b", 8, lambda C, a, b: C.compare(a, b, "GT", signed=True)),
+                            ("minimum", 8, lambda C, a, b: C.minmax(a, b)),
+                            ("divu 6-bit", 6, lambda C, a, b: C.divu(a, b))):
+        C = T.Circuit(); a, b = C.inputs(nb), C.inputs(nb); build(C, a, b)
+        x = r.integers(0, 2**nb, B); y = r.integers(1, 2**nb, B)
+        x[0] = 2**nb - 1
+        out.append((name, C, {**_bits(a, x, nb), **_bits(b, y, nb)}, B))
+    return out
+
+
+def test_circuits_every_wire_torus32_vs_oracle(ctx, okey, keyset, rng):
+    """Whole circuits Torus32-exact: every wire of config 3's 32-bit ripple-carry addition (depth
+    32) and of the 8x8 multiplier, signed comparison, minimum and 6-bit division, evaluated on the
+    GPU (level-batched rows, bootstrap-free nodes folded in) equals a node-by-node evaluation with
+    the exact oracle's bootstraps and key switches (tests/circuit_oracle.py), word for word."""
+    import circuit_oracle
+    torch = _torch()
+    for name, C, bits, B in _circuits_for_torus32():
+        n_w = C.info()["wires"]
+        enc = {w: keyset.encrypt(v, rng) for w, v in bits.items()}
+        wa = torch.zeros((n_w, B, n), dtype=torch.int32, device="cuda")
+        wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+        for w, (ea, eb) in enc.items():
+            wa[w] = torch.from_numpy(ea).cuda()
+            wb[w] = torch.from_numpy(eb).cuda()
+        C.run_dev(ctx, B, wa, wb)
+        torch.cuda.synchronize()
+        ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+        W = circuit_oracle.eval_circuit(C, okey, enc, B)
+        bad = [w for w in range(n_w) if not (np.array_equal(ha[w], W[w][0]) and np.array_equal(hb[w], W[w][1]))]
+        assert not bad, (name, bad[:10])
+        ref = C.eval_plain(bits)
+        for w in range(n_w):
+            dec = keyset.decrypt(ha[w], hb[w])
+            assert np.array_equal(dec, np.broadcast_to(ref[w], dec.shape)), (name, w)
+
+
 def test_circuit_rows_torus32_vs_oracle(ctx, okey, keyset, rng):
     """k_blind_rotate_v6_rows + the circuit key switch: each bootstrapped row's output equals
     the oracle's bootstrap + key switch of the same linear combination, word for word, for
