@@ -254,6 +254,37 @@ def test_circuits_every_wire_torus32_vs_oracle(ctx, okey, keyset, rng):
             assert np.array_equal(dec, np.broadcast_to(ref[w], dec.shape)), (name, w)
 
 
+def test_config4_mul_16x16_batch256_wires_torus32_sampled(ctx, okey, keyset, rng):
+    """configs[3] at its size (256 independent 16 x 16 products, 931 bootstraps each, one circuit
+    run): every wire of instances 0, 127 and 255 equals the exact oracle's node-by-node evaluation
+    of those instances word for word, and all 256 products decrypt right."""
+    import circuit_oracle
+    torch = _torch()
+    nb, B = 16, 256
+    C = T.Circuit()
+    a, b = C.inputs(nb), C.inputs(nb)
+    p = C.mul(a, b)
+    x = rng.integers(0, 2**nb, B)
+    y = rng.integers(0, 2**nb, B)
+    x[0], y[0] = 2**nb - 1, 2**nb - 1
+    bits = {**_bits(a, x, nb), **_bits(b, y, nb)}
+    n_w = C.info()["wires"]
+    enc = {w: keyset.encrypt(v, rng) for w, v in bits.items()}
+    wa = torch.zeros((n_w, B, n), dtype=torch.int32, device="cuda")
+    wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+    for w, (ea, eb) in enc.items():
+        wa[w] = torch.from_numpy(ea).cuda()
+        wb[w] = torch.from_numpy(eb).cuda()
+    C.run_dev(ctx, B, wa, wb)
+    torch.cuda.synchronize()
+    ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+    assert np.array_equal(T.int_of([keyset.decrypt(ha[w], hb[w]) for w in p]), x * y)
+    k = np.array([0, 127, 255])
+    W = circuit_oracle.eval_circuit(C, okey, {w: (ea[k], eb[k]) for w, (ea, eb) in enc.items()}, len(k))
+    bad = [w for w in range(n_w) if not (np.array_equal(ha[w][k], W[w][0]) and np.array_equal(hb[w][k], W[w][1]))]
+    assert not bad, bad[:10]
+
+
 def test_circuit_rows_torus32_vs_oracle(ctx, okey, keyset, rng):
     """k_blind_rotate_v6_rows + the circuit key switch: each bootstrapped row's output equals
     the oracle's bootstrap + key switch of the same linear combination, word for word, for
