@@ -190,6 +190,8 @@ struct TfheAmdContext {
     hipStream_t copy_in = nullptr;
     hipEvent_t ev_in = nullptr, ev_out[2] = {nullptr, nullptr};
     std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
+    void *mtab = nullptr;       // mixed-gate batches: device row / key-switch tables
+    size_t mtab_bytes = 0;
 };
 
 // Collects the launches of one C-ABI batch call into its context's last_kernels; nested calls
@@ -234,6 +236,9 @@ static int free_key(DeviceKey &k) {
 }
 
 static int free_scratch(TfheAmdContext *c) {
+    if (c->mtab) (void)hipFree(c->mtab);
+    c->mtab = nullptr;
+    c->mtab_bytes = 0;
     if (c->u_a) (void)hipFree(c->u_a);
     if (c->u_b) (void)hipFree(c->u_b);
     if (c->io) (void)hipFree(c->io);
@@ -751,6 +756,95 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     return TFHE_AMD_OK;
 }
 
+// B gates of mixed kinds (gates[i] = TFHE_GATE_NAND .. TFHE_GATE_MUX) in ONE blind-rotation launch
+// and ONE key-switch launch: the batch is a one-level circuit of one instance — wires 3i, 3i + 1,
+// 3i + 2 hold gate i's inputs a, b (, c), wire 3B + i its result; gate i contributes one row
+// (c, sa, sb) = its prologue (boot-gates.cu:98-397), a MUX two rows and a combined key switch
+// (:407-448), in request order (row r of the extracted samples: gate i's first row, then its
+// second for a MUX).  The rows kernel is the circuit path's k_blind_rotate_v6_rows, guarded.
+// cc_* may be null when no gate is a MUX.  res may alias inputs.
+extern "C" int tfhe_amd_gate_batch_mixed_host(TfheAmdContext *c, int B, const int *gates, int32_t *res_a,
+                                              int32_t *res_b, const int32_t *ca_a, const int32_t *ca_b,
+                                              const int32_t *cb_a, const int32_t *cb_b, const int32_t *cc_a,
+                                              const int32_t *cc_b) {
+    if (!c || B < 0) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!gates || !res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
+    if (!c->key.has_bk || !(c->key.ksk4 || c->key.ksk5)) return TFHE_AMD_E_ARG;
+    int nmux = 0;
+    for (int i = 0; i < B; ++i) {
+        int32_t k0, k1, k2;
+        if (gates[i] == TFHE_GATE_MUX) ++nmux;
+        else if (!gate_spec(gates[i], &k0, &k1, &k2)) return TFHE_AMD_E_ARG;
+    }
+    if (nmux && (!cc_a || !cc_b)) return TFHE_AMD_E_ARG;
+    const int rows = B + nmux;
+    std::vector<CircRow> rw((size_t)rows);
+    std::vector<CircKs> ks((size_t)B);
+    for (int i = 0, r = 0; i < B; ++i) {
+        if (gates[i] == TFHE_GATE_MUX) {
+            rw[r] = CircRow{-kMu, 1, 1, 0, 3 * i, 3 * i + 1, -1, 0};
+            rw[r + 1] = CircRow{-kMu, -1, 1, 0, 3 * i, 3 * i + 2, -1, 0};
+            ks[i] = CircKs{r, r + 1, kMu, 3 * B + i};
+            r += 2;
+        } else {
+            int32_t k0, k1, k2;
+            gate_spec(gates[i], &k0, &k1, &k2);
+            rw[r] = CircRow{k0, k1, k2, 0, 3 * i, 3 * i + 1, -1, 0};
+            ks[i] = CircKs{r, -1, 0, 3 * B + i};
+            r += 1;
+        }
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    TraceScope trace(c);
+    int rc = tfhe_amd_reserve(c, std::max(B, (rows + 1) / 2));   // u / guard scratch for `rows` rows
+    if (rc) return rc;
+    const size_t tab = sizeof(CircRow) * rw.size() + sizeof(CircKs) * ks.size();
+    if (tab > c->mtab_bytes) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->mtab) (void)hipFree(c->mtab);
+        c->mtab = nullptr;
+        c->mtab_bytes = 0;
+        HIPCHK(hipMalloc(&c->mtab, tab));
+        c->mtab_bytes = tab;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c->fence.acquire(s));
+    // wires: a [4B][500], b [4B] in the io scratch (4 cap x 501 words), staged the same way on the host
+    const size_t WA = (size_t)4 * B * kn;
+    int32_t *h = c->h_io, *d = c->io;
+    const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
+    for (int i = 0; i < B; ++i)
+        for (int k = 0; k < (gates[i] == TFHE_GATE_MUX ? 3 : 2); ++k) {
+            memcpy(h + (size_t)(3 * i + k) * kn, in_a[k] + (size_t)i * kn, kn * 4);
+            h[WA + 3 * i + k] = in_b[k][i];
+        }
+    HIPCHK(hipMemcpyAsync(d, h, (size_t)3 * B * kn * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d + WA, h + WA, (size_t)3 * B * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->mtab, rw.data(), sizeof(CircRow) * rw.size(), hipMemcpyHostToDevice, s));
+    const CircKs *d_ks = (const CircKs *)((char *)c->mtab + sizeof(CircRow) * rw.size());
+    HIPCHK(hipMemcpyAsync((void *)d_ks, ks.data(), sizeof(CircKs) * ks.size(), hipMemcpyHostToDevice, s));
+    {
+        ProfScope ps(c, s, true);
+        const Guard gd = ctx_guard(c);
+        HIPCHK(launch_blind_rotate_rows(c->key, 1, rows, (const CircRow *)c->mtab, d, d + WA, kMu, c->u_a, c->u_b, s,
+                                        &gd));
+    }
+    {
+        ProfScope ps(c, s, false);
+        HIPCHK(launch_keyswitch_rows(c->key, 1, B, d_ks, c->u_a, c->u_b, d, d + WA, s));
+    }
+    int32_t *hr = h + (size_t)3 * B * kn;
+    HIPCHK(hipMemcpyAsync(hr, d + (size_t)3 * B * kn, (size_t)B * kn * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + WA + 3 * B, d + WA + 3 * B, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c->fence.done(s));
+    HIPCHK(hipStreamSynchronize(s));   // also: the host tables above may be freed on return
+    memcpy(res_a, hr, (size_t)B * kn * 4);
+    memcpy(res_b, h + WA + 3 * B, (size_t)B * 4);
+    return TFHE_AMD_OK;
+}
+
 // woKS / bootstrap / KS host versions: same staging scheme (in-place safe)
 enum { OP_WOKS, OP_BOOT, OP_KS };
 static int single_input_host(TfheAmdContext *c, int op, int B, int32_t mu, const int32_t *in_a,
@@ -803,7 +897,7 @@ int tfhe_amd_internal_unsliced_max() { return host_slice() > 0 ? host_slice() : 
 // round (unsliced host path), halves x B rows of kN words: the Tier-1 API derives the
 // key-switched output's current_variance from their digits (tfhe_api.cpp ks_variance).
 int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a) {
-    if (!c || B <= 0 || halves < 1 || halves > 2 || B > c->cap) return TFHE_AMD_E_ARG;
+    if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap) return TFHE_AMD_E_ARG;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(u_a, c->u_a, sizeof(int32_t) * (size_t)halves * B * kN, hipMemcpyDeviceToHost));

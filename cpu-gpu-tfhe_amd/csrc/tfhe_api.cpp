@@ -776,10 +776,61 @@ static int coalesce_window_us() {
     return v;
 }
 
-// Runs one batch of queued gates on lane l: per gate kind one host batch (inputs staged before
-// anything is written, so a result may alias any input of its own call); each request gets its
-// key-switch input back, from which its caller sums current_variance as the single-gate path.
+// Runs one batch of queued gates on lane l: one gate kind -> one host gate batch, several kinds
+// -> one mixed launch (above); inputs are staged before anything is written, so a result may
+// alias any input of its own call; each request gets its key-switch input back, from which its
+// caller sums current_variance as the single-gate path.
+// A batch holding more than one gate kind runs as ONE mixed launch (tfhe_amd_gate_batch_mixed_host:
+// one blind rotation + one key switch for all kinds) in rounds of 512 gates.
+static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
+    std::vector<int32_t> buf, u;
+    std::vector<int> gates;
+    const int total = (int)batch.size();
+    for (int s0 = 0; s0 < total; s0 += 512) {
+        const int n = std::min(512, total - s0);
+        const size_t A = (size_t)n * kn;
+        buf.assign(4 * A + 4 * (size_t)n, 0);
+        int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
+        int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
+        gates.resize(n);
+        int rows = 0;
+        for (int i = 0; i < n; ++i) {
+            const Tier1Req *q = batch[s0 + i];
+            gates[i] = q->gate;
+            memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
+            memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
+            if (q->gate == TFHE_GATE_MUX) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
+            rows += q->gate == TFHE_GATE_MUX ? 2 : 1;
+        }
+        const int rc = tfhe_amd_gate_batch_mixed_host(l, n, gates.data(), ra, rb, aa, ab, ba, bb, ca, cb);
+        if (rc != TFHE_AMD_OK) {
+            for (int i = s0; i < total; ++i) batch[i]->rc = rc;
+            return;
+        }
+        u.resize((size_t)rows * kN);
+        check(tfhe_amd_internal_last_extracted(l, rows, 1, u.data()), "variance bookkeeping");
+        for (int i = 0, r = 0; i < n; ++i) {   // rows in request order: a MUX has two (u1 + u2)
+            Tier1Req *q = batch[s0 + i];
+            memcpy(q->r->a, ra + (size_t)i * kn, kn * 4);
+            q->r->b = rb[i];
+            q->u.assign(u.begin() + (size_t)r * kN, u.begin() + (size_t)(r + 1) * kN);
+            if (q->gate == TFHE_GATE_MUX) {
+                for (int j = 0; j < kN; ++j)
+                    q->u[j] = (int32_t)((uint32_t)q->u[j] + (uint32_t)u[(size_t)(r + 1) * kN + j]);
+                r += 2;
+            } else {
+                r += 1;
+            }
+        }
+    }
+}
+
 static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
+    for (const Tier1Req *q : batch)
+        if (q->gate != batch[0]->gate) {
+            run_tier1_mixed(l, batch);
+            return;
+        }
     std::vector<Tier1Req *> group;
     std::vector<int32_t> buf, u;
     std::vector<bool> taken(batch.size(), false);

@@ -62,6 +62,7 @@ def _load():
     for f in ("tfhe_amd_gate_batch_dev",):
         getattr(L, f).argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_VP] * 8 + [_VP]
     L.tfhe_amd_gate_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_I32P] * 8
+    L.tfhe_amd_gate_batch_mixed_host.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int)] + [_I32P] * 8
     L.tfhe_amd_bootstrap_woks_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
     L.tfhe_amd_bootstrap_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
     L.tfhe_amd_keyswitch_batch_dev.argtypes = [_VP, ctypes.c_int] + [_VP] * 4 + [_VP]
@@ -383,6 +384,18 @@ class Context:
                                             _p(i32(cb_a)), _p(i32(cb_b)),
                                             _p(None if cc_a is None else i32(cc_a)),
                                             _p(None if cc_b is None else i32(cc_b))), "gate_batch_host")
+        return r_a, r_b
+
+    def gate_mixed_host(self, gates, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None):
+        """tfhe_amd_gate_batch_mixed_host: gate i of kind gates[i] (names or codes) on row i, all in
+        one blind-rotation and one key-switch launch."""
+        g = np.array([GATES[x] if isinstance(x, str) else int(x) for x in gates], dtype=np.int32)
+        ca_a = i32(ca_a); B = ca_a.shape[0]
+        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        _check(lib.tfhe_amd_gate_batch_mixed_host(self.h, B, g.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _p(r_a),
+                                                  _p(r_b), _p(ca_a), _p(i32(ca_b)), _p(i32(cb_a)), _p(i32(cb_b)),
+                                                  _p(None if cc_a is None else i32(cc_a)),
+                                                  _p(None if cc_b is None else i32(cc_b))), "gate_batch_mixed_host")
         return r_a, r_b
 
     def woks_host(self, mu, x_a, x_b):

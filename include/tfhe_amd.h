@@ -83,6 +83,17 @@ int tfhe_amd_gate_batch_host(TfheAmdContext *ctx, int gate, int B,
                              const int32_t *cb_a, const int32_t *cb_b,
                              const int32_t *cc_a, const int32_t *cc_b);
 
+/* B gates of MIXED kinds (gates[i] = TFHE_GATE_NAND .. TFHE_GATE_MUX, a host array) in one
+ * blind-rotation launch and one key-switch launch (a one-level circuit: a MUX is two rows and a
+ * combined key switch); cc_* only read for MUX entries (may be NULL without one).  Host arrays,
+ * synchronous; res may alias inputs.  The Tier-1 coalescing queue runs its mixed batches
+ * through it. */
+int tfhe_amd_gate_batch_mixed_host(TfheAmdContext *ctx, int B, const int *gates,
+                                   int32_t *res_a, int32_t *res_b,
+                                   const int32_t *ca_a, const int32_t *ca_b,
+                                   const int32_t *cb_a, const int32_t *cb_b,
+                                   const int32_t *cc_a, const int32_t *cc_b);
+
 /* tfhe_bootstrap_woKS_FFT over B inputs x (n=500) -> u (N=1024): u_a [B][1024], u_b [B] */
 int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *ctx, int B, int32_t mu,
                                       const int32_t *x_a, const int32_t *x_b,

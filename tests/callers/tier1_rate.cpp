@@ -89,10 +89,38 @@ int main(int argc, char **argv) {
                  runs.empty() ? "" : ", ", T, n, dt, n / dt, bad, nb, nb ? (double)ng / nb : 0.0, big);
         runs += line;
     }
+    // mixed kinds: gate i is kind i mod 11 (the 10 binary gates and MUX), as threads of a real
+    // program that sit in different parts of their circuits; the largest team, in place on odd i
+    typedef void (*Gate2)(LweSample *, const LweSample *, const LweSample *, const TFheGateBootstrappingCloudKeySet *);
+    const Gate2 g2[10] = {bootsNAND, bootsOR, bootsAND, bootsXOR, bootsXNOR, bootsNOR, bootsANDNY, bootsANDYN,
+                          bootsORNY, bootsORYN};
+    auto mixed = [&](int i, LweSample *r, const LweSample *x) {
+        const int k = i % 11;
+        if (k < 10) g2[k](r, x, &b[i], bk);
+        else bootsMUX(r, x, &b[i], &a[(i + 1) % P], bk);
+    };
+    for (int i = 0; i < P; i++) mixed(i, &seq[i], &a[i]);
+    const int T = maxT, n = maxT * per_thread;
+    for (int i = 0; i < n; i++) lweCopy(&out[i], &a[i], lp);
+    tfhe_amd_tier1_queue_stats(bk, nullptr, nullptr, nullptr, 1);
+    t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(T) schedule(static)
+    for (int i = 0; i < n; i++) {
+        if (i & 1) mixed(i, &out[i], &out[i]);
+        else mixed(i, &out[i], &a[i]);
+    }
+    const double dt_mixed = omp_get_wtime() - t0;
+    long long nbm = 0, ngm = 0, bigm = 0;
+    tfhe_amd_tier1_queue_stats(bk, &nbm, &ngm, &bigm, 1);
+    int bad_mixed = 0;
+    for (int i = 0; i < n; i++) bad_mixed += !same(&out[i], &seq[i], dim);
+    mismatches += bad_mixed;
     const char *co = getenv("TFHE_AMD_TIER1_COALESCE");
     printf("{\"coalesce\": %s, \"pool\": %d, \"sequential_gates_per_s\": %.1f, \"truth_errors\": %d, "
-           "\"mismatches\": %d, \"runs\": [%s]}\n",
-           co && co[0] == '0' ? "false" : "true", P, P / seq_s, truth_errors, mismatches, runs.c_str());
+           "\"mismatches\": %d, \"runs\": [%s], \"mixed_kinds\": {\"threads\": %d, \"gates\": %d, "
+           "\"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, \"batches\": %lld, \"mean_batch\": %.2f}}\n",
+           co && co[0] == '0' ? "false" : "true", P, P / seq_s, truth_errors, mismatches, runs.c_str(), T, n,
+           dt_mixed, n / dt_mixed, bad_mixed, nbm, nbm ? (double)ngm / nbm : 0.0);
     delete_gate_bootstrapping_ciphertext_array(P, out);
     delete_gate_bootstrapping_ciphertext_array(P, seq);
     delete_gate_bootstrapping_ciphertext_array(P, b);

@@ -397,3 +397,33 @@ def test_fp64_ceiling_measurement():
     assert torch.cuda.current_device() == dev
     with pytest.raises(T.TfheAmdError):
         T.fp64_ceiling(0, 0, 1.0)
+
+
+@pytest.mark.gpu
+def test_mixed_gate_batch_bit_exact(ctx, okey, keyset, rng):
+    """tfhe_amd_gate_batch_mixed_host: all 11 gate kinds interleaved in one batch (one blind
+    rotation over 1 row per gate, 2 per MUX, one key switch) — every output equals the oracle's
+    gate of its kind word for word, for a small batch (one row per CU) and one above a round of
+    rows per CU (300 gates, ~330 rows: the register-rotation kernel), and decrypts right."""
+    names = ["NAND", "OR", "AND", "XOR", "XNOR", "NOR", "ANDNY", "ANDYN", "ORNY", "ORYN", "MUX"]
+    truth = {"NAND": lambda a, b, c: 1 - (a & b), "OR": lambda a, b, c: a | b, "AND": lambda a, b, c: a & b,
+             "XOR": lambda a, b, c: a ^ b, "XNOR": lambda a, b, c: 1 - (a ^ b), "NOR": lambda a, b, c: 1 - (a | b),
+             "ANDNY": lambda a, b, c: (1 - a) & b, "ANDYN": lambda a, b, c: a & (1 - b),
+             "ORNY": lambda a, b, c: (1 - a) | b, "ORYN": lambda a, b, c: a | (1 - b),
+             "MUX": lambda a, b, c: np.where(a == 1, b, c)}
+    for B in (37, 300):
+        gates = [names[i % len(names)] if i % 7 else names[rng.integers(0, len(names))] for i in range(B)]
+        xa, xb, xc = (rng.integers(0, 2, B) for _ in range(3))
+        (aa, ab), (ba, bb), (ca, cb) = (keyset.encrypt(v, rng) for v in (xa, xb, xc))
+        r_a, r_b = ctx.gate_mixed_host(gates, aa, ab, ba, bb, ca, cb)
+        assert "k_blind_rotate_v6_rows" in ",".join(ctx.last_kernels())
+        g = np.array(gates)
+        for name in names:
+            idx = np.flatnonzero(g == name)
+            if idx.size == 0:
+                continue
+            args = [aa[idx], ab[idx], ba[idx], bb[idx]] + ([ca[idx], cb[idx]] if name == "MUX" else [])
+            o_a, o_b = okey.gate_batch(name, *args)
+            assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b), (B, name)
+            want = truth[name](xa[idx], xb[idx], xc[idx])
+            assert np.array_equal(keyset.decrypt(r_a[idx], r_b[idx]), want), (B, name)

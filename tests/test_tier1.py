@@ -62,6 +62,8 @@ def test_tier1_coalescing_queue_rate():
         assert out["truth_errors"] == 0 and out["mismatches"] == 0, out
     rate = {r["threads"]: r["gates_per_s"] for r in q["runs"]}
     assert rate[64] >= 20 * rate[1], q
+    # mixed gate kinds (all 10 binary gates and MUX across the team): one launch per batch
+    assert q["mixed_kinds"]["mismatches"] == 0 and q["mixed_kinds"]["gates_per_s"] >= 10 * rate[1], q
     assert max(r["largest_batch"] for r in q["runs"]) > 1, q
 
 
