@@ -74,6 +74,11 @@ def parse():
     ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the sustained fp64 ceiling measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-multi", action="store_true",
+                    help="skip the one-process multi-device leg (only runs when several GPUs are visible)")
+    ap.add_argument("--multi-devices", default="",
+                    help="device slots of the one-process multi-device leg (default: every visible GPU; "
+                         "e.g. 0,0 rehearses two slots on one GPU)")
     ap.add_argument("--parity-samples", type=int, default=128,
                     help="outputs of the timed batch compared Torus32-for-Torus32 with the exact oracle")
     return ap.parse_args()
@@ -251,6 +256,43 @@ def sample_clock(device, run_step, seconds=2.0):
         return None
     samples.sort()
     return {"mhz": samples[len(samples) // 2], "samples": len(samples)}
+
+
+def multi_device_leg(T, torch, K, args, rng):
+    """B = args.batch gates per device on every visible device from this one process: a
+    MultiContext over all devices, each shard resident in its device's HBM, K steps of
+    multi.gate_dev + multi.sync timed; the NAND truth table of every shard checked after."""
+    devs = ([int(d) for d in args.multi_devices.split(",")] if args.multi_devices
+            else list(range(torch.cuda.device_count())))
+    n = len(devs)
+    m = T.MultiContext(K.bk, K.ksk, devs)
+    B = args.batch
+    shards, bits = [], []
+    for d in devs:
+        x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+        a_a, a_b = K.encrypt(x, rng)
+        b_a, b_b = K.encrypt(y, rng)
+        dev = [torch.from_numpy(v).to(f"cuda:{d}") for v in (a_a, a_b, b_a, b_b)]
+        r_a = torch.empty((B, 500), dtype=torch.int32, device=f"cuda:{d}")
+        r_b = torch.empty(B, dtype=torch.int32, device=f"cuda:{d}")
+        shards.append([r_a, r_b] + dev)
+        bits.append((x, y))
+    for _ in range(max(1, args.warmup)):
+        m.gate_dev(args.gate, shards)
+    m.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.gate_dev(args.gate, shards)
+    m.sync()
+    el = time.perf_counter() - t0
+    ok = None
+    if args.gate == "NAND":
+        ok = all(np.array_equal(K.decrypt(sh[0].cpu().numpy(), sh[1].cpu().numpy()), 1 - (x & y))
+                 for sh, (x, y) in zip(shards, bits))
+    m.close()
+    return {"devices": n, "batch_per_device": B, "steps": args.steps, "ms_per_step": el / args.steps * 1e3,
+            "value": n * B * args.steps / el, "truth_table_ok": ok,
+            "api": "tfhe_amd_multi_gate_batch_dev + tfhe_amd_multi_sync (one process, one key replica per device)"}
 
 
 def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
@@ -461,6 +503,12 @@ def main():
         line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
                           "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
                           "steps": steps, "truth_table_ok": ok}
+
+    # one process driving every visible GPU through the library (tfhe_amd_multi_gate_batch_dev:
+    # device-resident shards, one key replica per device, no collective) — what a C++ host such as
+    # cloud.cpp gets without torchrun; only when this single process sees several GPUs
+    if world == 1 and not args.no_multi and (torch.cuda.device_count() > 1 or args.multi_devices):
+        line["one_process_multi_device"] = multi_device_leg(T, torch, K, args, rng)
 
     gd, gr = ctx.guard_stats()
     line["guard"] = {"max_distance": gd, "recomputed": gr, "threshold": 0.125,
