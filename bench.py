@@ -508,7 +508,10 @@ def main():
     # device-resident shards, one key replica per device, no collective) — what a C++ host such as
     # cloud.cpp gets without torchrun; only when this single process sees several GPUs
     if world == 1 and not args.no_multi and (torch.cuda.device_count() > 1 or args.multi_devices):
-        line["one_process_multi_device"] = multi_device_leg(T, torch, K, args, rng)
+        try:
+            line["one_process_multi_device"] = multi_device_leg(T, torch, K, args, rng)
+        except Exception as e:   # a secondary leg: record it, never lose the headline line
+            line["one_process_multi_device"] = {"error": repr(e)[:500]}
 
     gd, gr = ctx.guard_stats()
     line["guard"] = {"max_distance": gd, "recomputed": gr, "threshold": 0.125,
