@@ -54,5 +54,10 @@ int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, in
                                   const int32_t *b_b, const int32_t *c_a, const int32_t *c_b);
 // the extracted samples of a context's last gate batch (<= one round), halves x B rows of 1024
 int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a);
+// device copy of host bytes on a context's GPU / its release; device-side current_variance of the
+// context's last gate batch (engine.cpp)
+int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev);
+void tfhe_amd_internal_free(int device, void *dev);
+int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out);
 // drops the multi-device context registered for a key (tfhe_gpu_init) when the key is deleted
 void tfhe_amd_internal_forget_multi(const void *bkfft);

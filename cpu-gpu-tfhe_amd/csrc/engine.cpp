@@ -904,6 +904,34 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
     return TFHE_AMD_OK;
 }
 
+// device copy of host data on a context's GPU (tfhe_api.cpp: the KSK row variances)
+int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev) {
+    if (!c || !host || !dev) return TFHE_AMD_E_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(dev, bytes));
+    HIPCHK(hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice));
+    return TFHE_AMD_OK;
+}
+void tfhe_amd_internal_free(int device, void *dev) {
+    if (!dev) return;
+    (void)hipSetDevice(device);
+    (void)hipFree(dev);
+}
+
+// current_variance of the context's last gate batch (<= one round: its key-switch inputs are still
+// in the scratch), computed on the device (k_ks_variance) into out [B]
+int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out) {
+    if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap || !d_var || !out)
+        return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(hipSetDevice(c->device));
+    double *d_out = reinterpret_cast<double *>(c->io);   // the batch's staging is done with by now
+    HIPCHK(launch_ks_variance(c->u_a, B, halves, d_var, d_out, c->stream));
+    HIPCHK(hipMemcpyAsync(out, d_out, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TFHE_AMD_OK;
+}
+
 // a second context on the same GPU sharing `primary`'s key (own stream + scratch):
 // used for per-thread lanes of the Tier-1 API
 TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {

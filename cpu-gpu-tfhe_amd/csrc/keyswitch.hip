@@ -786,6 +786,35 @@ hipError_t launch_ksk_to_v5(const int32_t *d_ksk, int32_t *d_ksk5, hipStream_t s
     return hipGetLastError();
 }
 
+// current_variance bookkeeping of B key-switched samples (tfhe_api.cpp tfhe_amd_boots_batch): per
+// sample the reference's sum over i < 1024, j < 8 of the variance of the key-switching-key row its
+// non-zero digit selects (lweKeySwitchTranslate_fromArray, lwe-keyswitch-functions.cu:101-127;
+// lwe-functions.cu:150), in the same i, j order with the same IEEE double adds, so the doubles
+// are the reference's.  One thread per sample (halves = 2: the MUX's u1 + u2).  var [1024][8][4].
+__global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ u_a, int B, int halves,
+                                                    const double *__restrict__ var, double *__restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B) return;
+    const int32_t *u = u_a + (size_t)g * kN;
+    const int32_t *u2 = halves == 2 ? u_a + ((size_t)B + g) * kN : nullptr;
+    double v = 0.0;
+    for (int i = 0; i < kN; ++i) {
+        const uint32_t aibar = (uint32_t)u[i] + (u2 ? (uint32_t)u2[i] : 0u) + kKsPrecOffset;
+#pragma unroll
+        for (int j = 0; j < kKsT; ++j) {
+            const uint32_t aij = (aibar >> (32 - (j + 1) * kKsBasebit)) & (uint32_t)(kKsBase - 1);
+            if (aij) v = __dadd_rn(v, var[(i * kKsT + j) * kKsBase + aij]);
+        }
+    }
+    out[g] = v;
+}
+
+hipError_t launch_ks_variance(const int32_t *u_a, int B, int halves, const double *var, double *out, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ks_variance, dim3((B + 63) / 64), dim3(64), 0, s, u_a, B, halves, var, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_circuit_linear(int B, int nlin, const CircLin *lin, int32_t *wa, int32_t *wb, hipStream_t s) {
     if (B <= 0 || nlin <= 0) return hipSuccess;
     const size_t total = (size_t)nlin * B * (kn + 1);

@@ -555,6 +555,7 @@ struct KeyEntry {
     std::mutex mu;
     Coalescer q;
     TfheAmdContext *qlane = nullptr;   // the coalescing queue's lane (used by one leader at a time)
+    double *d_var = nullptr;           // KSK row variances [1024][8][4] on the primary's device
 };
 static std::mutex g_reg_mu;
 static std::unordered_map<const void *, std::shared_ptr<KeyEntry>> g_reg;   // bkFFT or KSK -> entry
@@ -607,6 +608,8 @@ static void forget_device_keys(const void *k1, const void *k2) {
         e->lanes.clear();
         if (e->qlane) tfhe_amd_context_destroy(e->qlane);
         e->qlane = nullptr;
+        if (e->d_var) tfhe_amd_internal_free(tfhe_amd_context_device(e->primary), e->d_var);
+        e->d_var = nullptr;
         tfhe_amd_context_destroy(e->primary);
         e->primary = nullptr;
     }
@@ -1019,15 +1022,38 @@ EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a,
     // bookkeeping
     const int halves = gate == TFHE_GATE_MUX ? 2 : 1;
     const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
-    std::vector<int32_t> u;
+    // the KSK row variances on the device, once per key: each round's current_variance is then
+    // summed by k_ks_variance (the reference's order of double adds) instead of on the host from
+    // the round's 4 KB-per-gate key-switch inputs (B = 1024: ~16 ms of host work and a 4 MB copy)
+    double *d_var = nullptr;
+    {
+        std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
+        std::lock_guard<std::mutex> lk(e->mu);
+        if (!e->d_var) {
+            const LweKeySwitchKey *ks = bk->bkFFT->ks;
+            std::vector<double> var((size_t)kN * kKsT * kKsBase);
+            for (int i = 0; i < kN; ++i)
+                for (int j = 0; j < kKsT; ++j)
+                    for (int h = 0; h < kKsBase; ++h)
+                        var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
+            void *dv = nullptr;
+            const int rc = tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv);
+            if (rc) return rc;
+            e->d_var = (double *)dv;
+        }
+        d_var = e->d_var;
+    }
+    std::vector<double> v;
     for (int s0 = 0; s0 < B; s0 += round) {
         const int n = B - s0 < round ? B - s0 : round;
         const size_t o = (size_t)s0 * kn;
         int rc = tfhe_amd_gate_batch_host(l, gate, n, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
                                           c ? ca + o : nullptr, c ? cb + s0 : nullptr);
         if (rc) return rc;
-        ks_input_of_last(l, n, halves, u);
-        for (int i = 0; i < n; i++) result[s0 + i].current_variance = ks_variance(bk->bkFFT->ks, u.data() + (size_t)i * kN);
+        v.resize(n);
+        rc = tfhe_amd_internal_ks_variance(l, n, halves, d_var, v.data());
+        if (rc) return rc;
+        for (int i = 0; i < n; i++) result[s0 + i].current_variance = v[i];
     }
     for (int i = 0; i < B; i++) {
         memcpy(result[i].a, ra + (size_t)i * kn, kn * 4);

@@ -137,3 +137,64 @@ def test_tier1_current_variance_as_reference(keyset, okey, rng):
     usum = (u1[0].astype(np.int64) + u2[0]).astype(np.int64)
     assert s[3].current_variance == expected(usum)
     lib.delete_gate_bootstrapping_ciphertext_array(4, arr)
+
+
+@pytest.mark.gpu
+def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
+    """tfhe_amd_boots_batch over LweSample arrays (SURVEY.md §8(b)'s LweSample convenience overload):
+    1 100 NAND gates (two rounds: 1 024 + 76) and 33 MUX gates give the Torus32 words of the device
+    batch path, and current_variance — summed on the device by k_ks_variance in the reference's order
+    of double adds — equals, bit for bit, the Tier-1 gates' (summed on the host) on sampled rows."""
+    import ctypes
+    import time
+    import numpy as np
+    import tfhe_amd as T
+
+    class LweSample(ctypes.Structure):
+        _fields_ = [("a", ctypes.POINTER(ctypes.c_int32)), ("b", ctypes.c_int32), ("current_variance", ctypes.c_double)]
+    P = ctypes.c_void_p
+    lib = T.lib
+    lib.tfhe_amd_boots_batch.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P]
+    lib.bootsNAND.argtypes = [P, P, P, P]
+    lib.bootsMUX.argtypes = [P, P, P, P, P]
+    lib.new_gate_bootstrapping_ciphertext_array.restype = P
+    cloud = keyset.cloud
+
+    def arrays(B, n):
+        out = []
+        for _ in range(n):
+            p = lib.new_gate_bootstrapping_ciphertext_array(B, P(keyset.params))
+            out.append((p, (LweSample * B).from_address(p)))
+        return out
+
+    def fill(s, a, b):
+        for k in range(a.shape[0]):
+            ctypes.memmove(s[k].a, a[k].ctypes.data, 4 * 500)
+            s[k].b = int(b[k])
+
+    for gate, B in (("NAND", 1100), ("MUX", 33)):
+        nin = 3 if gate == "MUX" else 2
+        bits = [rng.integers(0, 2, B) for _ in range(nin)]
+        host = [keyset.encrypt(v, rng) for v in bits]
+        arrs = arrays(B, nin + 1)
+        for (p, s), (a, b) in zip(arrs[:nin], host):
+            fill(s, a, b)
+        res_p, res = arrs[nin]
+        t0 = time.perf_counter()
+        rc = lib.tfhe_amd_boots_batch(T.GATES[gate], P(res_p), P(arrs[0][0]), P(arrs[1][0]),
+                                      P(arrs[2][0]) if nin == 3 else None, B, P(cloud))
+        dt = time.perf_counter() - t0
+        assert rc == 0
+        got_a = np.array([np.ctypeslib.as_array(res[k].a, (500,)) for k in range(B)])
+        got_b = np.array([res[k].b for k in range(B)], dtype=np.int32)
+        want = ctx.gate_host(gate, *[v for hb in host for v in hb])
+        assert np.array_equal(got_a, want[0]) and np.array_equal(got_b, want[1]), gate
+        print(f"tfhe_amd_boots_batch {gate} B={B}: {dt * 1e3:.1f} ms")
+        one = arrays(1, 1)[0]
+        for k in np.unique(np.concatenate([[0, B - 1, min(1023, B - 1), min(1024, B - 1)],
+                                           rng.choice(B, 12, replace=False)])):
+            ins = [P(ctypes.addressof(arrs[j][1][k])) for j in range(nin)]
+            (lib.bootsMUX if gate == "MUX" else lib.bootsNAND)(P(one[0]), *ins, P(cloud))
+            assert one[1][0].current_variance == res[k].current_variance > 0, (gate, k)
+        for p, _ in arrs + [one]:
+            lib.delete_gate_bootstrapping_ciphertext_array(B if p != one[0] else 1, P(p))
