@@ -938,6 +938,16 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
 }
 
+// Builds the key's Tier-1 device context (key upload + conversion, HIP initialisation, the
+// queue's lane) now, so that the first gate call pays only its own latency.
+EXPORT int tfhe_amd_tier1_prepare(const TFheGateBootstrappingCloudKeySet *bk) {
+    if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
+    std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->qlane) e->qlane = tfhe_amd_context_lane(e->primary);
+    return e->qlane ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
+}
+
 EXPORT int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches,
                                       long long *gates, long long *largest, int reset) {
     if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;

@@ -206,6 +206,10 @@ int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
  * queue_stats: batches run, gates they held, the largest batch (reset = 1 zeroes them). */
 int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches, long long *gates,
                                long long *largest, int reset);
+/* Build the key's Tier-1 device context now (HIP initialisation, key upload and conversion on the
+ * device, the queue's stream and scratch: 0.1-0.3 s once per process and key) instead of inside
+ * the first gate call. */
+int tfhe_amd_tier1_prepare(const TFheGateBootstrappingCloudKeySet *bk);
 
 /* Device selection for the Tier-1 (single-gate) API: the GPU used by the cached
  * context of every cloud key (default 0). */
