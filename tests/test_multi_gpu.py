@@ -224,3 +224,44 @@ def test_two_ranks_scatter_gpu_gather():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert same and exact
+
+
+def test_multi_and_mixed_edge_cases(ctx, okey, keyset, rng):
+    """Edge shapes of the round-3 APIs: a device-resident multi batch whose second slot is empty, a
+    one-instance circuit over two slots (one idles), B = 0 everywhere, and mixed batches of a single
+    gate and of MUX only — all equal to the single-context path / the oracle."""
+    torch = _torch()
+    m = T.MultiContext(keyset.bk, keyset.ksk, [0, 0])
+    try:
+        B = 5
+        x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+        host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+        dev = [torch.from_numpy(v).cuda() for v in host]
+        r_a = torch.empty((B, 500), dtype=torch.int32, device="cuda")
+        r_b = torch.empty(B, dtype=torch.int32, device="cuda")
+        empty = [torch.empty((0, 500), dtype=torch.int32, device="cuda"), torch.empty(0, dtype=torch.int32, device="cuda")] * 3
+        m.gate_dev("AND", [[r_a, r_b] + dev, empty])
+        m.sync()
+        want = ctx.gate_host("AND", *host)
+        assert np.array_equal(r_a.cpu().numpy(), want[0]) and np.array_equal(r_b.cpu().numpy(), want[1])
+        m.gate_dev("AND", [empty, empty])                       # B = 0 on both slots
+        m.sync()
+        C = T.Circuit()
+        a, b = C.inputs(4), C.inputs(4)
+        s, co = C.add(a, b)
+        planes = T.bits_of(np.array([9]), 4) + T.bits_of(np.array([7]), 4)
+        enc = [keyset.encrypt(p, rng) for p in planes]
+        out_a, out_b = m.circuit_host(C, 1, a + b, np.stack([e[0] for e in enc]), np.stack([e[1] for e in enc]),
+                                      s + [co])
+        assert T.int_of([keyset.decrypt(out_a[k], out_b[k]) for k in range(5)])[0] == 16
+        z = np.zeros((0, 0, 500), np.int32)
+        m.circuit_host(C, 0, [], z, np.zeros((0, 0), np.int32), [])
+    finally:
+        m.close()
+    (sa, sb), (ua, ub), (va, vb) = (keyset.encrypt(rng.integers(0, 2, 3), rng) for _ in range(3))
+    got = ctx.gate_mixed_host(["MUX"] * 3, sa, sb, ua, ub, va, vb)
+    want = okey.gate_batch("MUX", sa, sb, ua, ub, va, vb)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    got1 = ctx.gate_mixed_host(["XNOR"], sa[:1], sb[:1], ua[:1], ub[:1])
+    want1 = okey.gate_batch("XNOR", sa[:1], sb[:1], ua[:1], ub[:1])
+    assert np.array_equal(got1[0], want1[0]) and np.array_equal(got1[1], want1[1])
