@@ -637,6 +637,7 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
 // another moves slice s - 1 out, and the host stages / unstages the pinned buffers meanwhile.
 // Same staging layout as below; slices touch disjoint rows, so a result that aliases an input
 // (the same array) is still read before it is written.
+
 static int host_slice() {   // TFHE_AMD_HOST_SLICE overrides (0: one unsliced batch)
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_HOST_SLICE");

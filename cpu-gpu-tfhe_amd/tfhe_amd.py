@@ -376,10 +376,16 @@ class Context:
         _check(lib.tfhe_amd_reserve(self.h, int(B)), "reserve")
 
     # ---- host (numpy) batches
-    def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None):
+    def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, out=None):
+        """tfhe_amd_gate_batch_host; out = (r_a [B][500], r_b [B]) int32 arrays to reuse (else new ones)."""
         g = GATES[gate] if isinstance(gate, str) else int(gate)
         ca_a = i32(ca_a); B = ca_a.shape[0]
-        r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
+        if out is not None:
+            r_a, r_b = out
+            if r_a.shape != (B, n_lwe) or r_b.shape != (B,) or r_a.dtype != np.int32 or r_b.dtype != np.int32:
+                raise TfheAmdError("out: need int32 arrays [B][500] and [B]")
+        else:
+            r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
         _check(lib.tfhe_amd_gate_batch_host(self.h, g, B, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)),
                                             _p(i32(cb_a)), _p(i32(cb_b)),
                                             _p(None if cc_a is None else i32(cc_a)),

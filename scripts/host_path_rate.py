@@ -19,12 +19,15 @@ for B in [int(b) for b in (sys.argv[1:] or ["1", "1024", "4096"])]:
     x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
     (a_a, a_b), (b_a, b_b) = K.encrypt(x, rng), K.encrypt(y, rng)
     ctx.reserve(B)
+    # results into reused, already-touched arrays (a C caller's buffers): fresh numpy arrays would
+    # add the first-touch page faults of B x 2 KB to every call
+    out = (np.zeros((B, 500), np.int32), np.zeros(B, np.int32))
     for _ in range(2):
-        r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b)
+        r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b, out=out)
     reps = 10
     t0 = time.perf_counter()
     for _ in range(reps):
-        r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b)
+        r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b, out=out)
     dt = (time.perf_counter() - t0) / reps
     ok = bool(np.array_equal(K.decrypt(r_a, r_b), 1 - (x & y)))
     # the same batch from HBM-resident inputs (device API), same process, for the overhead
