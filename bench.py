@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--multi-devices", default="",
                     help="device slots of the one-process multi-device leg (default: every visible GPU; "
                          "e.g. 0,0 rehearses two slots on one GPU)")
+    ap.add_argument("--multi-only", action="store_true", help=argparse.SUPPRESS)   # the child of run_multi_child
     ap.add_argument("--parity-samples", type=int, default=128,
                     help="outputs of the timed batch compared Torus32-for-Torus32 with the exact oracle")
     return ap.parse_args()
@@ -295,6 +296,38 @@ def multi_device_leg(T, torch, K, args, rng):
             "api": "tfhe_amd_multi_gate_batch_dev + tfhe_amd_multi_sync (one process, one key replica per device)"}
 
 
+def run_multi_child(args):
+    """The multi-device leg in a child process under a time limit, so that a fault or hang on a
+    many-GPU host costs that leg, never the headline line (the parent has synchronized its own
+    GPU work and waits idle)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--multi-only", "--batch", str(args.batch), "--steps",
+           str(args.steps), "--warmup", str(args.warmup), "--gate", args.gate]
+    if args.multi_devices:
+        cmd += ["--multi-devices", args.multi_devices]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"child exit {r.returncode}: {r.stderr[-400:]}"}
+    return json.loads(lines[-1])
+
+
+def multi_only(args):
+    import torch
+    import tfhe_amd as T
+    K = T.SecretKeyset()
+    try:
+        out = multi_device_leg(T, torch, K, args, np.random.default_rng(7000))
+    except Exception as e:
+        out = {"error": repr(e)[:500]}
+    print(json.dumps(out), flush=True)
+    K.close()
+
+
 def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
     """Torus32 parity of the timed batch itself: `nsamp` of its outputs (launch seams, rounds and
     a seeded random sample) against the exact CPU oracle (tests/oracle_ctypes.py, test-only
@@ -323,6 +356,8 @@ def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
 
 def main():
     args = parse()
+    if args.multi_only:
+        return multi_only(args)
     import torch
     import torch.distributed as dist
     import shard
@@ -508,10 +543,7 @@ def main():
     # device-resident shards, one key replica per device, no collective) — what a C++ host such as
     # cloud.cpp gets without torchrun; only when this single process sees several GPUs
     if world == 1 and not args.no_multi and (torch.cuda.device_count() > 1 or args.multi_devices):
-        try:
-            line["one_process_multi_device"] = multi_device_leg(T, torch, K, args, rng)
-        except Exception as e:   # a secondary leg: record it, never lose the headline line
-            line["one_process_multi_device"] = {"error": repr(e)[:500]}
+        line["one_process_multi_device"] = run_multi_child(args)
 
     gd, gr = ctx.guard_stats()
     line["guard"] = {"max_distance": gd, "recomputed": gr, "threshold": 0.125,

@@ -265,3 +265,20 @@ def test_multi_and_mixed_edge_cases(ctx, okey, keyset, rng):
     got1 = ctx.gate_mixed_host(["XNOR"], sa[:1], sb[:1], ua[:1], ub[:1])
     want1 = okey.gate_batch("XNOR", sa[:1], sb[:1], ua[:1], ub[:1])
     assert np.array_equal(got1[0], want1[0]) and np.array_equal(got1[1], want1[1])
+
+
+def test_bench_multi_device_leg_child_process():
+    """bench.py's one-process multi-device leg runs in a child process under a time limit (a fault
+    on a many-GPU host costs that leg, not the headline line): rehearsed here with two slots on
+    device 0, the child reports a rate and a correct NAND truth table on every shard."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--multi-only", "--multi-devices", "0,0",
+                        "--batch", "96", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, (r.returncode, r.stderr[-2000:])
+    out = json.loads(lines[-1])
+    assert out.get("devices") == 2 and out["truth_table_ok"] is True and out["value"] > 0, out
