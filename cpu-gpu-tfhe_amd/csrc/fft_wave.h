@@ -125,6 +125,17 @@ __device__ __forceinline__ Cx ld(const double2 *p) {
     const double2 v = *p;
     return Cx{v.x, v.y};
 }
+// FFT-domain key loads.  A/B variants (cache policy of the key stream, which every ciphertext
+// of the launch reads from L2): TFHE_AMD_V6_BK_NT = nontemporal loads (nt: bypass L1)
+__device__ __forceinline__ Cx ld_key(const double2 *p) {
+#ifdef TFHE_AMD_V6_BK_NT
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
+    return Cx{v.x, v.y};
+#else
+    return ld(p);
+#endif
+}
 __device__ __forceinline__ void st(double2 *p, const Cx &v) { *p = make_double2(v.re, v.im); }
 
 // per-lane twiddles of pass B (k = 0) or C (k = 1)
@@ -365,8 +376,8 @@ __device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c)
 #endif
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        b[0][r] = ld(bk + c * 512 + r * 64);
-        b[1][r] = ld(bk + (2 + c) * 512 + r * 64);
+        b[0][r] = ld_key(bk + c * 512 + r * 64);
+        b[1][r] = ld_key(bk + (2 + c) * 512 + r * 64);
     }
 }
 // Y = D_0 (x) BK[row 2w][c] + D_1 (x) BK[row 2w + 1][c], layout C
