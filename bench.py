@@ -297,7 +297,7 @@ def multi_device_leg(T, torch, K, args, rng):
 
 
 def run_multi_child(args):
-    """The multi-device leg in a child process under a time limit, so that a fault or hang on a
+    """The multi-device leg in a child process under a 150 s limit, so that a fault or hang on a
     many-GPU host costs that leg, never the headline line (the parent has synchronized its own
     GPU work and waits idle)."""
     import subprocess
@@ -307,9 +307,9 @@ def run_multi_child(args):
         cmd += ["--multi-devices", args.multi_devices]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env)
     except subprocess.TimeoutExpired:
-        return {"error": "timed out after 300 s"}
+        return {"error": "timed out after 150 s"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": f"child exit {r.returncode}: {r.stderr[-400:]}"}
