@@ -198,3 +198,61 @@ def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
             assert one[1][0].current_variance == res[k].current_variance > 0, (gate, k)
         for p, _ in arrs + [one]:
             lib.delete_gate_bootstrapping_ciphertext_array(B if p != one[0] else 1, P(p))
+
+
+@pytest.mark.gpu
+def test_tier1_raw_bootstrap_exports(keyset, okey, rng):
+    """The raw Tier-1 exports Cipher.cpp calls directly (addBitsRaw / bootsANDXOR, Cipher.cpp:647-766;
+    SURVEY.md §8(b)): tfhe_bootstrap_woKS_FFT (dimension-1 024 output), tfhe_bootstrap_FFT and
+    lweKeySwitch, through the C ABI on the key's own LweBootstrappingKeyFFT / LweKeySwitchKey
+    structs, against the exact oracle word for word — several mu (the gates' 1/8 and others), an
+    all-zero mask (identity CMux steps), modswitch edges, and tfhe_bootstrap_FFT with the result
+    aliasing its input."""
+    import ctypes
+    import numpy as np
+    import tfhe_amd as T
+
+    class LweSample(ctypes.Structure):
+        _fields_ = [("a", ctypes.POINTER(ctypes.c_int32)), ("b", ctypes.c_int32), ("current_variance", ctypes.c_double)]
+    P = ctypes.c_void_p
+    lib = T.lib
+    lib.tfhe_bootstrap_woKS_FFT.argtypes = [P, P, ctypes.c_int32, P]
+    lib.tfhe_bootstrap_FFT.argtypes = [P, P, ctypes.c_int32, P]
+    lib.lweKeySwitch.argtypes = [P, P, P]
+    bkfft = P.from_address(keyset.cloud + 16).value          # cloud->bkFFT
+    ks = P.from_address(bkfft + 40).value                    # bkFFT->ks
+
+    def sample(n, a=None, b=0):
+        buf = np.zeros(n, np.int32) if a is None else np.ascontiguousarray(a, dtype=np.int32).copy()
+        s = LweSample()
+        s.a = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        s.b = int(b)
+        return s, buf
+
+    bits = rng.integers(0, 2, 6)
+    x_a, x_b = keyset.encrypt(bits, rng)
+    x_a = x_a.copy()
+    x_a[3, :] = 0                                    # every rotation amount 0 (identity CMux steps)
+    x_a[4, :4] = [1 << 21, -(1 << 21), 2**31 - 1, -(2**31)]   # modswitch edges
+    mus = [1 << 29, -(1 << 29), 1 << 30, 123456789]
+    for k in range(x_a.shape[0]):
+        mu = mus[k % len(mus)]
+        xs, _ = sample(500, x_a[k], x_b[k])
+        # woKS: the extracted dimension-1 024 sample
+        u, ubuf = sample(1024)
+        lib.tfhe_bootstrap_woKS_FFT(P(ctypes.addressof(u)), P(bkfft), mu, P(ctypes.addressof(xs)))
+        w_a, w_b = okey.woks_batch(mu, x_a[k:k + 1], x_b[k:k + 1])
+        assert np.array_equal(ubuf, w_a[0]) and u.b == int(w_b[0]), ("woKS", k)
+        # full bootstrap = woKS + key switch
+        r, rbuf = sample(500)
+        lib.tfhe_bootstrap_FFT(P(ctypes.addressof(r)), P(bkfft), mu, P(ctypes.addressof(xs)))
+        k_a, k_b = okey.keyswitch_batch(w_a, w_b)
+        assert np.array_equal(rbuf, k_a[0]) and r.b == int(k_b[0]), ("bootstrap", k)
+        # the standalone key switch on the woKS output
+        r2, r2buf = sample(500)
+        lib.lweKeySwitch(P(ctypes.addressof(r2)), P(ks), P(ctypes.addressof(u)))
+        assert np.array_equal(r2buf, k_a[0]) and r2.b == int(k_b[0]), ("lweKeySwitch", k)
+        # result aliasing the input sample
+        xa, xabuf = sample(500, x_a[k], x_b[k])
+        lib.tfhe_bootstrap_FFT(P(ctypes.addressof(xa)), P(bkfft), mu, P(ctypes.addressof(xa)))
+        assert np.array_equal(xabuf, k_a[0]) and xa.b == int(k_b[0]), ("aliased bootstrap", k)
