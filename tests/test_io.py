@@ -262,3 +262,20 @@ def test_reference_callers_gpu(tmp_path):
     assert out["prod"] == (a & 0xFF) * (b & 0xFF)
     assert out["min"] == min(a, b)
     assert out["eq"] == 0 and out["gt"] == 1
+
+
+def test_host_api_surface_streams_and_helpers():
+    """The host-side TFHE API a libtfhe user may call beyond the reference's callers
+    (tests/callers/api_misc.cpp, built by __graft_entry__.build() against include/ + the library):
+    the std::stream writers give the FILE* writers' bytes and read back to identical keys / samples
+    (parameter set, secret and cloud keysets, gate ciphertexts, single LweSamples), the
+    allocators, lweClear, lweSymEncryptWithExternalNoise (phase = message + dtot32(noise), as
+    lwe-functions.cu:53-64) and t32tod."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "callers", "_bin", "api_misc")
+    if not os.access(exe, os.X_OK):
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe))])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (r.returncode, r.stderr[-2000:])
+    out = json.loads(lines[-1])
+    assert r.returncode == 0 and out["failed"] == 0, out
