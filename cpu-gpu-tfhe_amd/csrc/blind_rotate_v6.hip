@@ -149,7 +149,8 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
 template <int WAVES, bool RREG>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
-                                        int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi V6_STAMPS_PARAM) {
+                                        int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
+                                        uint32_t &bad V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
@@ -264,11 +265,18 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         load_C(sh.X[1 - own], o, L);
 #endif
         SCHED_FENCE();
-        mac6(D, bv, Y);
+        // throughput launches: the partner's partial sum seeds the second MAC (16 fp64 fewer per
+        // wave-step: B = 512 / 1 024 / 4 096 -0.9 / -0.8 / -0.6 %, profiles/r03_seed_mac2_ab.txt);
+        // the latency launches keep the MAC ahead of the partner loads' wait (B = 1: 1.69 -> 1.65 ms)
+        if constexpr (RREG) {
+            mac6_seeded(D, bv, o, Y);
+        } else {
+            mac6(D, bv, Y);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            Y[r].re += o[r].re;
-            Y[r].im += o[r].im;
+            for (int r = 0; r < 8; ++r) {
+                Y[r].re += o[r].re;
+                Y[r].im += o[r].im;
+            }
         }
     }
     pass_dit_C(Y);
@@ -339,7 +347,17 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
             acc[r + 8] += (uint32_t)__double_as_longlong(Y[r].im + 0x1.8p52);
         }
     }
+#elif defined(TFHE_AMD_V6_QGUARD)
+    // the rule on every coefficient (bad); the distance itself on one coefficient per lane and
+    // step, for the statistic (tfhe_amd_guard_stats)
+    mx = __builtin_fmax(mx, __builtin_fabs(Y[0].re - __builtin_rint(Y[0].re)));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        acc[r] += torus_of_qchk(Y[r].re, bad, hlo, hhi);
+        acc[r + 8] += torus_of_qchk(Y[r].im, bad, hlo, hhi);
+    }
 #else
+    (void)bad;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
@@ -400,7 +418,12 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
 #endif
     const int prio = g.prio;
     double mx = 0.0;                     // largest rounding distance of this lane (guard)
+#ifdef TFHE_AMD_V6_QGUARD
+    uint32_t hlo = kQShiftHiLo, hhi = kQShiftHiLo;   // range of the rounding shifter's high word (guard)
+#else
     uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;   // range of the rounding shifter's high word (guard)
+#endif
+    uint32_t bad = 0;                    // QGUARD: some coefficient's round(4c) != 0 mod 4
     int a_next = sh.bara[0];
     int own = w;                         // this wave's LDS buffer (the waves swap every step)
     for (int i = 0; i < kn; ++i) {
@@ -416,10 +439,14 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
+#ifdef TFHE_AMD_V6_QGUARD
+        if (bad || hlo < kQShiftHiLo || hhi >= kQShiftHiEnd) mx = 0.5;   // a distance >= 1/8, or |c| >= 2^49
+#else
         if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
+#endif
         const uint32_t h = wave_max_hi(mx);
         if (L == 0) {
             g.flags[2 * slot + w] = h;
@@ -544,8 +571,8 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         V6Stamps stamps;
 #endif
         double mx = 0.0;
-        uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
-        cmux_v6<2, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi V6_STAMPS_ARG);
+        uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo, bad = 0;
+        cmux_v6<2, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll

@@ -338,6 +338,23 @@ __device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx, uint32_t 
     return (uint32_t)__double_as_longlong(y);
 }
 
+// A/B (TFHE_AMD_V6_QGUARD): the 1/8 rule without the distance arithmetic.  y = c + 1.5 * 2^50
+// has ulp 1/4 while |c| < 2^49, so its low mantissa bits are round(4c): round(4c) = 0 mod 4 iff
+// |c - rint(c)| < 1/8 (ties aside), and mantissa bits 2..33 are then rint(c) mod 2^32.  Per
+// coefficient: one fp64 add, an alignbit, an and-or into `bad`, the min / max of the high word
+// (range: [2^50, 2^51)), instead of 3 fp64 adds and a max.
+constexpr uint32_t kQShiftHiLo = 0x43100000u;   // high word of 2^50
+constexpr uint32_t kQShiftHiEnd = 0x43200000u;  // high word of 2^51
+__device__ __forceinline__ uint32_t torus_of_qchk(double c, uint32_t &bad, uint32_t &hlo, uint32_t &hhi) {
+    const double y = c + 0x1.8p50;
+    const unsigned long long yb = (unsigned long long)__double_as_longlong(y);
+    const uint32_t lo = (uint32_t)yb, hy = (uint32_t)(yb >> 32);
+    bad |= lo & 3u;
+    hlo = hy < hlo ? hy : hlo;
+    hhi = hy > hhi ? hy : hhi;
+    return __builtin_amdgcn_alignbit(hy, lo, 2);
+}
+
 // high word of a non-negative double: monotone in its value, max-reduced across the wave
 __device__ __forceinline__ uint32_t wave_max_hi(double v) {
     uint32_t h = (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32);
@@ -381,6 +398,23 @@ __device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c)
     }
 }
 // Y = D_0 (x) BK[row 2w][c] + D_1 (x) BK[row 2w + 1][c], layout C
+// Y = o + sum_p D_p b_p: the second MAC seeded with the partner wave's partial sum (its first
+// products become FMAs and the 16 partial-sum adds disappear)
+__device__ __forceinline__ void mac6_seeded(const Cx (&D)[2][8], const Cx (&b)[2][8], const Cx (&o)[8], Cx (&Y)[8]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const Cx &b0 = b[0][r], &b1 = b[1][r];
+        double re = fma_(D[0][r].re, b0.re, o[r].re);
+        double im = fma_(D[0][r].re, b0.im, o[r].im);
+        re = fma_(-D[0][r].im, b0.im, re);
+        im = fma_(D[0][r].im, b0.re, im);
+        re = fma_(D[1][r].re, b1.re, re);
+        im = fma_(D[1][r].re, b1.im, im);
+        re = fma_(-D[1][r].im, b1.im, re);
+        im = fma_(D[1][r].im, b1.re, im);
+        Y[r] = Cx{re, im};
+    }
+}
 __device__ __forceinline__ void mac6(const Cx (&D)[2][8], const Cx (&b)[2][8], Cx (&Y)[8]) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
