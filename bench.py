@@ -547,9 +547,10 @@ def main():
 
     gd, gr = ctx.guard_stats()
     line["guard"] = {"max_distance": gd, "recomputed": gr, "threshold": 0.125,
-                     "what": "largest rounding distance |c - rint(c)| over every external-product coefficient of "
-                             "every bootstrap this process ran (all legs), and the ciphertexts the exact kernel "
-                             "recomputed (DESIGN.md 3.1)"}
+                     "what": "largest rounding distance |c - rint(c)| over the sampled external-product "
+                             "coefficients (one per lane and CMux step) of every bootstrap this process ran (all "
+                             "legs; the 1/8 rule itself is checked on every coefficient), and the ciphertexts the "
+                             "exact kernel recomputed (DESIGN.md 3.1)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(K.bk, K.ksk, rec["inputs"], rec["outputs"], args.cpu_seconds)
         parity["vs_cpu_port"] = line["cpu_baseline"]["outputs_vs_gpu"]

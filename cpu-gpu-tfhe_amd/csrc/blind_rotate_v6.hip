@@ -332,6 +332,7 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im); mx tracks the
     // rounding distance for the exactness guard
 #ifdef TFHE_AMD_V6_GUARD_HALF
+    (void)bad;
     // A/B experiment: measure the real parts on even steps and the imaginary parts on odd ones
     // (every coefficient every other step; half the guard's VALU)
     if (i & 1) {
@@ -347,21 +348,23 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
             acc[r + 8] += (uint32_t)__double_as_longlong(Y[r].im + 0x1.8p52);
         }
     }
-#elif defined(TFHE_AMD_V6_QGUARD)
-    // the rule on every coefficient (bad); the distance itself on one coefficient per lane and
-    // step, for the statistic (tfhe_amd_guard_stats)
-    mx = __builtin_fmax(mx, __builtin_fabs(Y[0].re - __builtin_rint(Y[0].re)));
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        acc[r] += torus_of_qchk(Y[r].re, bad, hlo, hhi);
-        acc[r + 8] += torus_of_qchk(Y[r].im, bad, hlo, hhi);
-    }
-#else
+#elif defined(TFHE_AMD_V6_DISTGUARD)
+    // A/B: round 2's form — the distance |c - rint(c)| of every coefficient (3 fp64 + a max)
     (void)bad;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
         acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
+    }
+#else
+    // the 1/8 rule on every coefficient through the quarter-ulp shifter (bad, fft_wave.h
+    // torus_of_qchk: B = 1 024 / 4 096 -0.9 / -1.1 %, profiles/r03_qguard_ab.txt); the distance
+    // itself on one coefficient per lane and step, for the statistic (tfhe_amd_guard_stats)
+    mx = __builtin_fmax(mx, __builtin_fabs(Y[0].re - __builtin_rint(Y[0].re)));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        acc[r] += torus_of_qchk(Y[r].re, bad, hlo, hhi);
+        acc[r + 8] += torus_of_qchk(Y[r].im, bad, hlo, hhi);
     }
 #endif
     wave_sync();
@@ -418,12 +421,12 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
 #endif
     const int prio = g.prio;
     double mx = 0.0;                     // largest rounding distance of this lane (guard)
-#ifdef TFHE_AMD_V6_QGUARD
-    uint32_t hlo = kQShiftHiLo, hhi = kQShiftHiLo;   // range of the rounding shifter's high word (guard)
-#else
+#if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
     uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;   // range of the rounding shifter's high word (guard)
+#else
+    uint32_t hlo = kQShiftHiLo, hhi = kQShiftHiLo;   // range of the rounding shifter's high word (guard)
 #endif
-    uint32_t bad = 0;                    // QGUARD: some coefficient's round(4c) != 0 mod 4
+    uint32_t bad = 0;                    // some coefficient's round(4c) != 0 mod 4 (distance >= 1/8)
     int a_next = sh.bara[0];
     int own = w;                         // this wave's LDS buffer (the waves swap every step)
     for (int i = 0; i < kn; ++i) {
@@ -442,10 +445,10 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
         cmux_v6<WAVES, RREG>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
-#ifdef TFHE_AMD_V6_QGUARD
-        if (bad || hlo < kQShiftHiLo || hhi >= kQShiftHiEnd) mx = 0.5;   // a distance >= 1/8, or |c| >= 2^49
-#else
+#if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
         if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
+#else
+        if (bad || hlo < kQShiftHiLo || hhi >= kQShiftHiEnd) mx = 0.5;   // a distance >= 1/8, or |c| >= 2^49
 #endif
         const uint32_t h = wave_max_hi(mx);
         if (L == 0) {

@@ -338,11 +338,14 @@ __device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx, uint32_t 
     return (uint32_t)__double_as_longlong(y);
 }
 
-// A/B (TFHE_AMD_V6_QGUARD): the 1/8 rule without the distance arithmetic.  y = c + 1.5 * 2^50
+// The rounding of the default kernel (round 3): the 1/8 rule without the distance arithmetic.  y = c + 1.5 * 2^50
 // has ulp 1/4 while |c| < 2^49, so its low mantissa bits are round(4c): round(4c) = 0 mod 4 iff
 // |c - rint(c)| < 1/8 (ties aside), and mantissa bits 2..33 are then rint(c) mod 2^32.  Per
 // coefficient: one fp64 add, an alignbit, an and-or into `bad`, the min / max of the high word
-// (range: [2^50, 2^51)), instead of 3 fp64 adds and a max.
+// (range: [2^50, 2^51)), instead of 3 fp64 adds and a max (torus_of_chk above, kept for the
+// experimental v8 and the TFHE_AMD_V6_DISTGUARD A/B build).  Real keys give |c| < 2^48 (the
+// product's sigma is 2^44.4); |c| >= 2^49 falls outside the shifter's binade and is flagged.
+// tests/test_guard.py emulates these operations.
 constexpr uint32_t kQShiftHiLo = 0x43100000u;   // high word of 2^50
 constexpr uint32_t kQShiftHiEnd = 0x43200000u;  // high word of 2^51
 __device__ __forceinline__ uint32_t torus_of_qchk(double c, uint32_t &bad, uint32_t &hlo, uint32_t &hhi) {

@@ -143,7 +143,8 @@ def test_guard_catches_worst_case_key(keyset, rng):
 
 
 def _torus_of_chk(c):
-    """numpy restatement of csrc/fft_wave.h torus_of_chk (IEEE double, the kernel's ops):
+    """numpy restatement of csrc/fft_wave.h torus_of_chk (IEEE double; round 2's rounding, kept in
+    the TFHE_AMD_V6_DISTGUARD A/B build and the experimental v8):
     returns (low word of y, rounding distance |c - q|, high word of y)."""
     c = np.asarray(c, dtype=np.float64)
     M2 = np.float64(1.5 * 2.0**52)
@@ -174,6 +175,45 @@ def test_single_shifter_rounding_exact_or_flagged():
     small = np.abs(c) < 2.0**51
     assert not flagged[small & (np.abs(c - np.rint(c)) < 0.125)].any()
     assert flagged[(c == -2.0**51 - 1) | (c == 2.0**51 + 1) | (c == 2.0**52)].all()   # the high-word checks
+
+
+def _torus_of_qchk(c):
+    """numpy restatement of csrc/fft_wave.h torus_of_qchk (the default kernel's rounding, IEEE
+    double): returns (rint(c) mod 2^32 as the kernel extracts it — mantissa bits 2..33 of
+    y = c + 1.5 * 2^50 —, round(4c) mod 4 = the low two bits, the high word of y)."""
+    c = np.asarray(c, dtype=np.float64)
+    y = c + np.float64(1.5 * 2.0**50)
+    bits = y.view(np.uint64)
+    return (((bits >> np.uint64(2)) & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+            (bits & np.uint64(3)).astype(np.uint32), (bits >> np.uint64(32)).astype(np.uint32))
+
+
+def test_quarter_shifter_rounding_exact_or_flagged():
+    """The default kernel's rounding (one 1.5 * 2^50 shifter, ulp 1/4): over the whole product range
+    |c| <= 2^52 the extracted word is rint(c) mod 2^32 or the coefficient is flagged (low bits
+    != 0: distance >= 1/8; or the high word outside [hi(2^50), hi(2^51)), i.e. |c| >= 2^49); every
+    coefficient within 1/8 of an integer and below 2^49 passes, and every one farther than 1/8
+    is flagged — the 1/8 rule of DESIGN.md §3.1 on every coefficient."""
+    r = np.random.default_rng(11)
+    mags = np.concatenate([r.uniform(-2.0**47, 2.0**47, 20000),
+                           r.uniform(-2.0**52, 2.0**52, 20000),
+                           r.uniform(2.0**48, 2.0**50, 5000) * r.choice([-1, 1], 5000)])
+    fr = r.uniform(-0.49, 0.49, mags.shape)
+    c = np.floor(mags) + fr
+    edges = np.array([2.0**49 - 1, 2.0**49, 2.0**49 + 1, 2.0**49 - 0.5, -2.0**49, -2.0**49 - 1,
+                      -2.0**49 + 0.25, 2.0**52, -2.0**52, 0.49, -0.49, 0.124, -0.124, 0.126, 0.0,
+                      7.875, 7.87, 2.0**31, -2.0**31 - 0.3])
+    c = np.concatenate([c, edges])
+    low, q4, hy = _torus_of_qchk(c)
+    want = (np.vectorize(lambda v: int(np.rint(v)) % 2**32)(c)).astype(np.uint32)
+    flagged = (q4 != 0) | (hy < 0x43100000) | (hy >= 0x43200000)
+    assert np.array_equal(low[~flagged], want[~flagged])
+    small = np.abs(c) < 2.0**49
+    dist = np.abs(c - np.rint(c))
+    assert not flagged[small & (dist < 0.125)].any()
+    assert flagged[small & (dist > 0.125)].all()
+    assert flagged[np.abs(c) > 2.0**49].all()                     # the high-word checks
+    assert flagged.sum() > 5000 and (~flagged).sum() > 5000
 
 
 _ADV = r"""
