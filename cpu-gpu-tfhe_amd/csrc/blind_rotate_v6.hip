@@ -147,7 +147,7 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
-template <int WAVES, bool RREG>
+template <int WAVES, bool RREG, bool RSW = false>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
                                         uint32_t &bad V6_STAMPS_PARAM) {
@@ -193,13 +193,40 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         uint32_t V[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) V[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)acc[r]);
-        if (q & 16) {
+        // RSW (the one-ciphertext-per-workgroup kernels of launches above 2 ciphertexts per CU,
+        // i.e. the throughput launches): one of 32 static register permutations chosen by a scalar branch
+        // tree on q — 16 moves / negations instead of up to 5 conditional stages of 16 (B = 1 024
+        // / 4 096 -0.5 / -0.35 %; at B = 512, one wave per SIMD, the branch tree on the critical
+        // path costs +1 %, so the paired kernel keeps the stages: profiles/r03_rswitch_ab.txt)
+        if constexpr (RSW) {
+            uint32_t O[16];
+            switch (q) {
+#define V6_ROT_CASE(Q)                                                                            \
+    case Q: {                                                                                     \
+        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                          \
+            const int k = r - (Q);                                                                \
+            O[r] = k >= 0 ? V[k] : (k >= -16 ? 0u - V[k + 16] : V[k + 32]);                       \
+        }                                                                                         \
+    } break;
+                V6_ROT_CASE(0) V6_ROT_CASE(1) V6_ROT_CASE(2) V6_ROT_CASE(3) V6_ROT_CASE(4) V6_ROT_CASE(5)
+                V6_ROT_CASE(6) V6_ROT_CASE(7) V6_ROT_CASE(8) V6_ROT_CASE(9) V6_ROT_CASE(10) V6_ROT_CASE(11)
+                V6_ROT_CASE(12) V6_ROT_CASE(13) V6_ROT_CASE(14) V6_ROT_CASE(15) V6_ROT_CASE(16) V6_ROT_CASE(17)
+                V6_ROT_CASE(18) V6_ROT_CASE(19) V6_ROT_CASE(20) V6_ROT_CASE(21) V6_ROT_CASE(22) V6_ROT_CASE(23)
+                V6_ROT_CASE(24) V6_ROT_CASE(25) V6_ROT_CASE(26) V6_ROT_CASE(27) V6_ROT_CASE(28) V6_ROT_CASE(29)
+                V6_ROT_CASE(30)
+                default: V6_ROT_CASE(31)
+#undef V6_ROT_CASE
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) V[r] = O[r];
+        }
+        if (!RSW && (q & 16)) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) V[r] = 0u - V[r];
         }
 #pragma unroll
         for (int K = 8; K >= 1; K >>= 1) {
-            if (q & K) {
+            if (!RSW && (q & K)) {
                 uint32_t t[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) t[r] = r >= K ? V[r - K] : 0u - V[r + 16 - K];
@@ -442,7 +469,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG, RREG && C == 1>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
 #if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
@@ -575,7 +602,9 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
 #endif
         double mx = 0.0;
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo, bad = 0;
-        cmux_v6<2, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad V6_STAMPS_ARG);
+        // RREG: the throughput launches' form (the scalar-branch permutation, RSW), so that the
+        // forced rotation edges of test_register_rotation_edges reach it
+        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll

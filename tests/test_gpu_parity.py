@@ -349,8 +349,9 @@ print("ks-v4 ok", c.key_bytes())
 def test_register_rotation_subprocess():
     """TFHE_AMD_V6_RREG=1 (read once per process) forces the register / ds_bpermute rotation of
     cmux_v6 — the default only above one workgroup per CU — onto small launches: the CMux steps
-    at the rotation edges (a = 0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048) and woKS with
-    bara = 0 runs still equal the oracle."""
+    at the rotation edges (a = 0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048), every register
+    shift q = a >> 6 of the throughput kernels' 32-way permutation, and woKS with bara = 0 runs
+    still equal the oracle."""
     import subprocess
     import sys
     code = r"""
@@ -359,11 +360,14 @@ sys.path[:0] = [%r, %r]
 import tfhe_amd as T, oracle_ctypes as O
 K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); o = O.OracleKey(K.bk, K.ksk)
 rng = np.random.default_rng(5)
-B, iters = 4, 10
+B, iters = 4, 32
 acc0 = rng.integers(-2**31, 2**31, (B, 2, 1024), dtype=np.int64).astype(np.int32)
 bara = rng.integers(0, 2049, (B, iters), dtype=np.int64).astype(np.int32)
-bara[0] = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048]
-bara[1] = [127, 128, 129, 960, 1087, 1088, 1984, 2000, 31, 32]
+bara[0, :10] = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048]
+bara[1, :10] = [127, 128, 129, 960, 1087, 1088, 1984, 2000, 31, 32]
+q = np.arange(32)
+bara[2] = 64 * q + np.mod(7 * q, 64)     # every register shift q with assorted lane shifts
+bara[3] = 64 * q + 63 - q
 d_acc = torch.from_numpy(acc0.copy()).cuda()
 c.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), iters); c.sync()
 got = d_acc.cpu().numpy()
