@@ -292,19 +292,10 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         load_C(sh.X[1 - own], o, L);
 #endif
         SCHED_FENCE();
-        // throughput launches: the partner's partial sum seeds the second MAC (16 fp64 fewer per
-        // wave-step: B = 512 / 1 024 / 4 096 -0.9 / -0.8 / -0.6 %, profiles/r03_seed_mac2_ab.txt);
-        // the latency launches keep the MAC ahead of the partner loads' wait (B = 1: 1.69 -> 1.65 ms)
-        if constexpr (RREG) {
-            mac6_seeded(D, bv, o, Y);
-        } else {
-            mac6(D, bv, Y);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                Y[r].re += o[r].re;
-                Y[r].im += o[r].im;
-            }
-        }
+        // the partner's partial sum seeds the second MAC (16 fp64 fewer per wave-step: B = 1 / 256
+        // / 512 / 1 024 / 4 096 -0.9 / -1.2 / -0.9 / -0.8 / -0.6 %, profiles/r03_seed_mac2_ab.txt,
+        // r03_seed_mac2_latency_ab.txt)
+        mac6_seeded(D, bv, o, Y);
     }
     pass_dit_C(Y);
     const Tw4 tB = TW7(tw7_invB);
