@@ -239,17 +239,17 @@ int tfhe_amd_select_kernel(int br_version);
  * the checked outputs. */
 int tfhe_amd_last_kernels(TfheAmdContext *ctx, char *buf, int cap);
 
-/* Exactness guard of the default fp64 FFT blind rotation: every launch
- * measures, per ciphertext, the largest distance |c - rint(c)| of every rounded external-product
- * coefficient over its 500 steps, and the range |c| < 2^51 of the rounding shifter; a ciphertext
- * at or above the threshold (default 1/8), or out of range, is recomputed by the exact 2-prime
- * NTT kernel in the same stream before its key switch.  The rule is statistical, not a proof: a
+/* Exactness guard of the default fp64 FFT blind rotation: every launch checks
+ * every rounded external-product coefficient of every ciphertext over its 500 steps against
+ * |c - rint(c)| < 1/8 (through the rounding shifter's quarter-ulp bits) and |c| < 2^49; a
+ * ciphertext that breaks either (or whose sampled distance reaches a lower threshold set below)
+ * is recomputed by the exact 2-prime NTT kernel in the same stream before its key switch.  The rule is statistical, not a proof: a
  * wrong coefficient needs an FFT error >= 1/2, and one that shows a distance < 1/8 needs >= 7/8
  * while all ~10^6 other roundings of that ciphertext stay below 1/8 (real keys: largest
  * distance 0.06-0.08, FFT errors of one step spread over all its coefficients).  guard_stats reads (and optionally resets)
- * the context's largest measured distance and its count of recomputed ciphertexts (it
- * synchronizes the device).  set_guard_threshold is process-wide (0 recomputes everything:
- * tests). */
+ * the context's largest distance over the sampled coefficients (one per lane and CMux step) and
+ * its count of recomputed ciphertexts (it synchronizes the device).  set_guard_threshold is
+ * process-wide (0 recomputes everything: tests; thresholds above 1/8 leave the 1/8 check). */
 int tfhe_amd_guard_stats(TfheAmdContext *ctx, double *max_distance, long long *recomputed, int reset);
 int tfhe_amd_set_guard_threshold(double distance);
 
