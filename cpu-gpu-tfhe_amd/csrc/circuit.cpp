@@ -59,10 +59,8 @@ struct CircuitDevState {
     StreamFence fence;   // u scratch reuse across caller streams
     ~CircuitDevState() { release(); }
     void release() {
-        if (dev >= 0) {
-            (void)hipSetDevice(dev);
-            (void)hipDeviceSynchronize();   // a run on a caller's stream may still read them
-        }
+        DeviceScope dev_scope(dev);   // the frees below are on dev; the caller keeps its device
+        if (dev >= 0) (void)hipDeviceSynchronize();   // a run on a caller's stream may still read them
         fence.release();
         if (d_tab) (void)hipFree(d_tab);
         if (u_a) (void)hipFree(u_a);

@@ -220,7 +220,7 @@ struct TraceScope {
     } while (0)
 
 static int free_key(DeviceKey &k) {
-    if (k.device >= 0) (void)hipSetDevice(k.device);
+    DeviceScope dev_scope(k.device);
     if (k.bk_ntt) (void)hipFree(k.bk_ntt);
     if (k.bk_v2) (void)hipFree(k.bk_v2);
     if (k.bk_fft) (void)hipFree(k.bk_fft);
@@ -257,7 +257,8 @@ int tfhe_amd_reserve(TfheAmdContext *c, int B) {
     if (B <= c->cap) return TFHE_AMD_OK;
     int cap = c->cap ? c->cap : 64;
     while (cap < B) cap *= 2;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipDeviceSynchronize());   // the scratch may still be in use on a caller's stream
     free_scratch(c);
     HIPCHK(hipMalloc(&c->u_a, sizeof(int32_t) * 2 * (size_t)cap * kN));
@@ -276,7 +277,8 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
     if (device < 0 || device >= ndev) return TFHE_AMD_E_ARG;
     c->device = device;
     c->key.device = device;
-    HIPCHK(hipSetDevice(device));
+    DeviceScope dev_scope(device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&c->gstats, sizeof(uint32_t) * 4));
     HIPCHK(hipMemset(c->gstats, 0, sizeof(uint32_t) * 4));
@@ -370,7 +372,7 @@ extern "C" int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk
 
 extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     if (!c) return TFHE_AMD_OK;
-    if (c->device >= 0) (void)hipSetDevice(c->device);
+    DeviceScope dev_scope(c->device);
     (void)hipDeviceSynchronize();   // work on caller streams may still use the scratch
     for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     for (auto &p : c->ks_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -410,7 +412,8 @@ extern "C" void *tfhe_amd_context_stream(TfheAmdContext *c) { return c ? (void *
 
 extern "C" int tfhe_amd_sync(TfheAmdContext *c) {
     if (!c) return TFHE_AMD_E_ARG;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipStreamSynchronize(c->stream));
     return TFHE_AMD_OK;
 }
@@ -434,7 +437,7 @@ static void prof_collect(TfheAmdContext *c) {
 
 extern "C" int tfhe_amd_profile_enable(TfheAmdContext *c, int enable) {
     if (!c) return TFHE_AMD_E_ARG;
-    (void)hipSetDevice(c->device);
+    DeviceScope dev_scope(c->device);
     prof_collect(c);
     c->prof = enable != 0;
     c->br_ms = c->ks_ms = 0;
@@ -444,7 +447,7 @@ extern "C" int tfhe_amd_profile_enable(TfheAmdContext *c, int enable) {
 
 extern "C" int tfhe_amd_profile_read(TfheAmdContext *c, double *br_ms, int *br_n, double *ks_ms, int *ks_n) {
     if (!c) return TFHE_AMD_E_ARG;
-    (void)hipSetDevice(c->device);
+    DeviceScope dev_scope(c->device);
     prof_collect(c);
     if (br_ms) *br_ms = c->br_ms;
     if (br_n) *br_n = c->br_n;
@@ -516,7 +519,8 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     if (B == 0) return TFHE_AMD_OK;
     if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
@@ -557,7 +561,8 @@ extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32
     if (B == 0) return TFHE_AMD_OK;
     if (!x_a || !x_b || !u_a || !u_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);   // guard flags live in the context's scratch
     if (rc) return rc;
@@ -578,7 +583,8 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     if (B == 0) return TFHE_AMD_OK;
     if (!x_a || !x_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
@@ -601,7 +607,8 @@ extern "C" int tfhe_amd_keyswitch_batch_dev(TfheAmdContext *c, int B, const int3
     if (B == 0) return TFHE_AMD_OK;
     if (!u_a || !u_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     ProfScope ps(c, s, false);
     HIPCHK(launch_keyswitch(c->key, B, u_a, u_b, nullptr, nullptr, 0, res_a, res_b, s));
@@ -614,7 +621,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     if (B == 0) return TFHE_AMD_OK;
     if (!acc || (iters > 0 && !bara)) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     ProfScope ps(c, s, true);
     const int v = br_version();
@@ -717,7 +725,8 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     }
     if (!c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
@@ -797,7 +806,8 @@ extern "C" int tfhe_amd_gate_batch_mixed_host(TfheAmdContext *c, int B, const in
         }
     }
     std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, std::max(B, (rows + 1) / 2));   // u / guard scratch for `rows` rows
     if (rc) return rc;
@@ -854,7 +864,8 @@ static int single_input_host(TfheAmdContext *c, int op, int B, int32_t mu, const
     if (B == 0) return TFHE_AMD_OK;
     if (!in_a || !in_b || !out_a || !out_b) return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
@@ -899,7 +910,8 @@ int tfhe_amd_internal_unsliced_max() { return host_slice() > 0 ? host_slice() : 
 // key-switched output's current_variance from their digits (tfhe_api.cpp ks_variance).
 int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a) {
     if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap) return TFHE_AMD_E_ARG;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(u_a, c->u_a, sizeof(int32_t) * (size_t)halves * B * kN, hipMemcpyDeviceToHost));
     return TFHE_AMD_OK;
@@ -908,14 +920,15 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
 // device copy of host data on a context's GPU (tfhe_api.cpp: the KSK row variances)
 int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev) {
     if (!c || !host || !dev) return TFHE_AMD_E_ARG;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipMalloc(dev, bytes));
     HIPCHK(hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice));
     return TFHE_AMD_OK;
 }
 void tfhe_amd_internal_free(int device, void *dev) {
     if (!dev) return;
-    (void)hipSetDevice(device);
+    DeviceScope dev_scope(device);
     (void)hipFree(dev);
 }
 
@@ -925,7 +938,8 @@ int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const do
     if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap || !d_var || !out)
         return TFHE_AMD_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     double *d_out = reinterpret_cast<double *>(c->io);   // the batch's staging is done with by now
     HIPCHK(launch_ks_variance(c->u_a, B, halves, d_var, d_out, c->stream));
     HIPCHK(hipMemcpyAsync(out, d_out, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
@@ -940,7 +954,8 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
     c->device = primary->device;
     c->key = primary->key;
     c->shared_key = true;
-    if (hipSetDevice(c->device) != hipSuccess ||
+    DeviceScope dev_scope(c->device);
+    if (dev_scope.rc != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->gstats, sizeof(uint32_t) * 4) != hipSuccess ||
         hipMemset(c->gstats, 0, sizeof(uint32_t) * 4) != hipSuccess ||
@@ -961,7 +976,8 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
     if (B == 0) return TFHE_AMD_OK;
     if (!wires_a || !wires_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     TraceScope trace(c);
     std::lock_guard<std::mutex> lk(c->mu);
     return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b, c->gstats);
@@ -977,7 +993,8 @@ extern "C" int tfhe_amd_set_guard_threshold(double distance) {
 
 extern "C" int tfhe_amd_guard_stats(TfheAmdContext *c, double *max_distance, long long *recomputed, int reset) {
     if (!c || !c->gstats) return TFHE_AMD_E_ARG;
-    HIPCHK(hipSetDevice(c->device));
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
     HIPCHK(hipDeviceSynchronize());   // launches on caller streams update the counters
     uint32_t h[4];
     HIPCHK(hipMemcpy(h, c->gstats, sizeof h, hipMemcpyDeviceToHost));

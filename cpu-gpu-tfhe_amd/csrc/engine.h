@@ -50,6 +50,24 @@ struct CircLin {
     int32_t c, s, in, out;
 };
 
+// Makes `device` current for the scope of an entry point and gives the caller's current device
+// back at its end: a caller that works on another GPU (torch.cuda.set_device(1), then a
+// context on device 0) keeps its own current device, which HIP and torch allocate on.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t rc;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        rc = device >= 0 && device != prev ? hipSetDevice(device) : hipSuccess;
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
+
 // Orders the reuse of a scratch buffer across streams.  Device-API callers may pass a different
 // stream per call; a call on another stream than the previous user's waits (on the device) for
 // the event recorded after that user's last launch, so two batches in flight never share the

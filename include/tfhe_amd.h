@@ -17,6 +17,8 @@
  * engine orders the reuse of its scratch between them.  A context serves one host thread at
  * a time (the Tier-1 API gives every calling thread its own lane).  `_host` functions take
  * host pointers and are synchronous.
+ * A call makes its context's device current only while it runs: the calling thread's current
+ * HIP device (the one torch and hipMalloc use) is the same after the call as before.
  * Every function returns 0 on success or a negative TFHE_AMD_E* code.
  */
 #ifndef TFHE_AMD_H

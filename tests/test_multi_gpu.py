@@ -62,6 +62,28 @@ def test_multi_context_all_visible_devices(keyset, rng):
         m.close()
 
 
+def test_library_calls_keep_the_callers_current_device(keyset, rng):
+    """Every entry point makes its context's device current only for the call (DeviceScope,
+    engine.h): a caller working on another GPU keeps its current device, which torch and HIP
+    allocate on.  On one GPU the call must leave device 0 current."""
+    torch = _torch()
+    n = torch.cuda.device_count()
+    mine = n - 1   # the caller's device; the context lives on device 0
+    torch.cuda.set_device(mine)
+    c = T.Context(keyset.bk, keyset.ksk, device=0)
+    try:
+        B = 5
+        x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+        got = c.gate_host("AND", *(keyset.encrypt(x, rng) + keyset.encrypt(y, rng)))
+        assert np.array_equal(keyset.decrypt(*got), x & y)
+        assert torch.cuda.current_device() == mine
+        assert torch.empty(1, device="cuda").device.index == mine
+    finally:
+        c.close()
+        assert torch.cuda.current_device() == mine
+        torch.cuda.set_device(0)
+
+
 def test_tfhe_gpu_init_and_boots_batch(ctx, keyset, rng):
     """tfhe_gpu_boots_batch before (Tier-1 device) and after tfhe_gpu_init (multi-device
     context over the visible GPUs) gives the same samples as the device context."""
