@@ -68,7 +68,7 @@ def parse():
                     help="untimed steps first: the clock and power state settle within ~10 (2: -2 %%)")
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
-    ap.add_argument("--extra-batches", default="1,4096", help="per-GPU batch sizes also timed ('none' = none)")
+    ap.add_argument("--extra-batches", default="1,512,4096", help="per-GPU batch sizes also timed ('none' = none)")
     ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
@@ -164,8 +164,12 @@ def cpu_baseline(bk, ksk, inputs, gpu_out, target_s):
         dt, _ = run(0, B, threads)
         t += dt
         n += B
+    # single-core figure: 32 bootstraps per sample, median of 5 samples (a 2 x 4 sample varied
+    # 7.8-10.5 ms box to box in round 3); the spread of the 5 is reported beside it
     run(0, 1, 1)
-    single = min(run(0, 4, 1)[0] / 4 for _ in range(2))
+    n1 = min(B, 32)
+    singles = sorted(run(0, n1, 1)[0] / n1 for _ in range(5))
+    single = singles[2]
     share = cpu_share()
     out = {"value": n / t, "unit": "gate bootstraps/s", "cores": threads, "kind": "port",
            "sample": f"the timed GPU batch's {B} bootsNAND inputs, {n // B} pass(es) = {n} bootstraps on "
@@ -174,6 +178,9 @@ def cpu_baseline(bk, ksk, inputs, gpu_out, target_s):
                      "algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to the exact oracle)",
            "same_inputs_as_gpu": True, "outputs_vs_gpu": {"checked": B, "mismatches": mismatches},
            "single_core_ms_per_bootstrap": single * 1e3,
+           "single_core_sample": {"bootstraps": n1, "samples": 5, "statistic": "median",
+                                  "min_ms": singles[0] * 1e3, "max_ms": singles[-1] * 1e3},
+           "per_thread_ms_per_bootstrap": threads * t / n * 1e3,
            "paper_single_core_ms_per_gate": 43.8,
            "max_round_error": fk.max_round_error(),
            "thread_cap": share,

@@ -61,3 +61,6 @@ void tfhe_amd_internal_free(int device, void *dev);
 int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out);
 // drops the multi-device context registered for a key (tfhe_gpu_init) when the key is deleted
 void tfhe_amd_internal_forget_multi(const void *bkfft);
+// circuit.cpp: drops every circuit's device state (tables, scratch) held for a context; called by
+// tfhe_amd_context_destroy (context uids are never reused, so a later context cannot inherit it)
+void tfhe_amd_internal_circuits_forget_context(unsigned long long ctx_uid);

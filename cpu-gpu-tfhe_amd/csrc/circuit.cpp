@@ -20,10 +20,12 @@
 #include <memory>
 #include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "engine.h"
 #include "../../include/tfhe_amd.h"
+#include "api_internal.h"
 
 using namespace tfhe_amd;
 
@@ -82,8 +84,31 @@ struct TfheAmdCircuit {
     int n_boot = 0, max_rows = 0;
     // per executing context (keyed by the context): device tables + scratch
     std::mutex mu;   // compile + the state map; runs on distinct contexts proceed concurrently
-    std::unordered_map<const void *, std::unique_ptr<CircuitDevState>> states;
+    // keyed by the context's uid (engine.cpp; never reused), dropped when the context is destroyed
+    std::unordered_map<uint64_t, std::unique_ptr<CircuitDevState>> states;
 };
+
+namespace {
+// every live circuit, so that a context's destruction can drop its states (lock order: this
+// registry, then a circuit's mu)
+std::mutex g_circuits_mu;
+std::unordered_set<TfheAmdCircuit *> g_circuits;
+}  // namespace
+
+void tfhe_amd_internal_circuits_forget_context(unsigned long long ctx_uid) {
+    std::vector<std::unique_ptr<CircuitDevState>> dead;
+    {
+        std::lock_guard<std::mutex> reg(g_circuits_mu);
+        for (TfheAmdCircuit *c : g_circuits) {
+            std::lock_guard<std::mutex> lk(c->mu);
+            auto it = c->states.find((uint64_t)ctx_uid);
+            if (it == c->states.end()) continue;
+            dead.push_back(std::move(it->second));
+            c->states.erase(it);
+        }
+    }
+    dead.clear();   // frees the device memory (CircuitDevState::release) outside the locks
+}
 
 namespace {
 
@@ -235,12 +260,27 @@ int add_node(TfheAmdCircuit *C, const Node &n) {
 extern "C" int tfhe_amd_circuit_create(TfheAmdCircuit **out) {
     if (!out) return TFHE_AMD_E_ARG;
     *out = new TfheAmdCircuit();
+    std::lock_guard<std::mutex> reg(g_circuits_mu);
+    g_circuits.insert(*out);
     return TFHE_AMD_OK;
 }
 
 extern "C" int tfhe_amd_circuit_destroy(TfheAmdCircuit *c) {
+    if (!c) return TFHE_AMD_OK;
+    {
+        std::lock_guard<std::mutex> reg(g_circuits_mu);
+        g_circuits.erase(c);
+    }
     delete c;
     return TFHE_AMD_OK;
+}
+
+// number of contexts a circuit currently holds device state for (tests: state is dropped with
+// its context)
+extern "C" int tfhe_amd_circuit_state_count(TfheAmdCircuit *c) {
+    if (!c) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return (int)c->states.size();
 }
 
 extern "C" int tfhe_amd_circuit_inputs(TfheAmdCircuit *c, int count) {
@@ -317,7 +357,7 @@ extern "C" int tfhe_amd_circuit_level_sizes(TfheAmdCircuit *c, int *rows_per_lev
 // wires_a [n_wires][B][500], wires_b [n_wires][B] on the context's device; input wires filled.
 // The circuit's structure must not change while runs are in flight (builders invalidate the
 // compiled schedule); runs on distinct contexts may overlap.
-int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
+int tfhe_amd_circuit_run_dev_impl(uint64_t ctx_uid, const DeviceKey &key, int device, hipStream_t s,
                                   TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb, uint32_t *guard_stats) {
     CircuitDevState *st;
     {
@@ -327,7 +367,7 @@ int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int
             if (rc != TFHE_AMD_OK) return rc;
             c->states.clear();   // tables of an earlier schedule
         }
-        auto &slot = c->states[ctx];
+        auto &slot = c->states[ctx_uid];
         if (!slot) slot.reset(new CircuitDevState());
         st = slot.get();
     }

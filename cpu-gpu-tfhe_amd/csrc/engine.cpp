@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "api_internal.h"
 #include "ntt_tables.h"
 #include "../../include/tfhe_amd.h"
 
@@ -164,6 +165,11 @@ using namespace tfhe_amd;
 
 // ------------------------------------------------------------------ context
 
+static uint64_t next_context_uid() {
+    static std::atomic<uint64_t> n{1};
+    return n.fetch_add(1, std::memory_order_relaxed);
+}
+
 struct TfheAmdContext {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -183,7 +189,10 @@ struct TfheAmdContext {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> br_ev, ks_ev;
     double br_ms = 0, ks_ms = 0;
     int br_n = 0, ks_n = 0;
-    std::mutex mu;
+    // host-side state of the context (scratch, staging, trace string, events): every entry point
+    // holds it; recursive because the host paths call the device entry points
+    std::recursive_mutex mu;
+    uint64_t uid = next_context_uid();   // never reused (circuit device states are keyed by it)
     bool shared_key = false;   // lane: the key belongs to another context
     StreamFence fence;         // u_a / u_b reuse across caller streams
     // sliced host batches (gate_batch_host_sliced): the input copy stream and the events
@@ -372,6 +381,7 @@ extern "C" int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk
 
 extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     if (!c) return TFHE_AMD_OK;
+    tfhe_amd_internal_circuits_forget_context(c->uid);   // circuits' device state for this context
     DeviceScope dev_scope(c->device);
     (void)hipDeviceSynchronize();   // work on caller streams may still use the scratch
     for (auto &p : c->br_ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -437,6 +447,7 @@ static void prof_collect(TfheAmdContext *c) {
 
 extern "C" int tfhe_amd_profile_enable(TfheAmdContext *c, int enable) {
     if (!c) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     prof_collect(c);
     c->prof = enable != 0;
@@ -447,6 +458,7 @@ extern "C" int tfhe_amd_profile_enable(TfheAmdContext *c, int enable) {
 
 extern "C" int tfhe_amd_profile_read(TfheAmdContext *c, double *br_ms, int *br_n, double *ks_ms, int *ks_n) {
     if (!c) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     prof_collect(c);
     if (br_ms) *br_ms = c->br_ms;
@@ -519,6 +531,7 @@ extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32
     if (B == 0) return TFHE_AMD_OK;
     if (!res_a || !res_b || !ca_a || !ca_b || !cb_a || !cb_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -561,6 +574,7 @@ extern "C" int tfhe_amd_bootstrap_woks_batch_dev(TfheAmdContext *c, int B, int32
     if (B == 0) return TFHE_AMD_OK;
     if (!x_a || !x_b || !u_a || !u_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -583,6 +597,7 @@ extern "C" int tfhe_amd_bootstrap_batch_dev(TfheAmdContext *c, int B, int32_t mu
     if (B == 0) return TFHE_AMD_OK;
     if (!x_a || !x_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -607,6 +622,7 @@ extern "C" int tfhe_amd_keyswitch_batch_dev(TfheAmdContext *c, int B, const int3
     if (B == 0) return TFHE_AMD_OK;
     if (!u_a || !u_b || !res_a || !res_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -621,6 +637,7 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     if (B == 0) return TFHE_AMD_OK;
     if (!acc || (iters > 0 && !bara)) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -724,7 +741,7 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
         if (!mux && !gate_spec(gate, &k0, &k1, &k2)) return TFHE_AMD_E_ARG;
     }
     if (!c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -805,7 +822,7 @@ extern "C" int tfhe_amd_gate_batch_mixed_host(TfheAmdContext *c, int B, const in
             r += 1;
         }
     }
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -863,7 +880,7 @@ static int single_input_host(TfheAmdContext *c, int op, int B, int32_t mu, const
     if (!c || B < 0) return TFHE_AMD_E_ARG;
     if (B == 0) return TFHE_AMD_OK;
     if (!in_a || !in_b || !out_a || !out_b) return TFHE_AMD_E_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
@@ -937,7 +954,7 @@ void tfhe_amd_internal_free(int device, void *dev) {
 int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out) {
     if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap || !d_var || !out)
         return TFHE_AMD_E_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     double *d_out = reinterpret_cast<double *>(c->io);   // the batch's staging is done with by now
@@ -967,7 +984,7 @@ TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
 }
 
 // circuit.cpp
-int tfhe_amd_circuit_run_dev_impl(TfheAmdContext *ctx, const DeviceKey &key, int device, hipStream_t s,
+int tfhe_amd_circuit_run_dev_impl(uint64_t ctx_uid, const DeviceKey &key, int device, hipStream_t s,
                                   TfheAmdCircuit *c, int B, int32_t *wa, int32_t *wb, uint32_t *guard_stats);
 
 extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ, int B, int32_t *wires_a,
@@ -976,11 +993,11 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
     if (B == 0) return TFHE_AMD_OK;
     if (!wires_a || !wires_b) return TFHE_AMD_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
     TraceScope trace(c);
-    std::lock_guard<std::mutex> lk(c->mu);
-    return tfhe_amd_circuit_run_dev_impl(c, c->key, c->device, s, circ, B, wires_a, wires_b, c->gstats);
+    return tfhe_amd_circuit_run_dev_impl(c->uid, c->key, c->device, s, circ, B, wires_a, wires_b, c->gstats);
 }
 
 extern "C" int tfhe_amd_set_guard_threshold(double distance) {
@@ -1011,6 +1028,7 @@ extern "C" int tfhe_amd_guard_stats(TfheAmdContext *c, double *max_distance, lon
 
 extern "C" int tfhe_amd_last_kernels(TfheAmdContext *c, char *buf, int cap) {
     if (!c || !buf || cap <= 0) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     const size_t n = std::min(c->last_kernels.size(), (size_t)cap - 1);
     memcpy(buf, c->last_kernels.data(), n);
     buf[n] = 0;

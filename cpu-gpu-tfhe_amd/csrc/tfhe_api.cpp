@@ -522,6 +522,7 @@ struct Tier1Req {
     int gate;
     LweSample *r;
     const LweSample *a, *b, *c;
+    bool taken = false;   // in a running batch
     bool done = false;
     int rc = TFHE_AMD_OK;
     std::vector<int32_t> u;   // its key-switch input: the caller derives current_variance from it
@@ -530,21 +531,30 @@ struct Tier1Req {
 // Coalescing queue of the Tier-1 gates of one key ("per-thread streams or a
 // batching queue").  The reference's CPU callers enter single gates from OpenMP teams
 // (Cipher.cpp:83-120, cloud.cpp:389-395); one B = 1 launch per call would occupy 2 waves of one
-// CU each, and a process has only 4 hardware queues.  Here a call enqueues its gate; whichever
-// waiting thread finds no batch running becomes the leader, takes every pending gate (grouped by
-// gate kind) and runs them as one batch per kind on the queue's lane, while the gates that arrive
-// meanwhile queue up for the next batch (group commit).  Before it takes them the leader waits
-// until every thread inside a gate call has enqueued (threads whose gate just completed either
-// come back with their next gate or leave), at most `window` (TFHE_AMD_TIER1_WINDOW_US): so an
-// OpenMP team's gates of one iteration go out as one batch.  A lone thread is its own leader at
-// once: its B = 1 latency is the plain path's.
+// CU each, and a process has only 4 hardware queues.  Here a call enqueues its gate; a waiting
+// thread becomes the leader of the next batch when a queue lane is free and no other leader is
+// collecting: it waits until every thread inside a gate call and not already in a running batch
+// has enqueued (at most the adaptive window below), takes every pending gate and runs them on
+// that lane — one gate kind as a gate batch, several kinds as one mixed launch per 512 gates.
+// Two lanes (own stream + scratch each) alternate, so batch k + 1 is staged and launched while
+// batch k is still on the GPU or being unstaged: the queue no longer serialises a whole batch's
+// host work with the next one.  A lone thread is its own leader at once (B = 1 latency).
+// The window adapts to the callers: it starts at TFHE_AMD_TIER1_WINDOW_US (default 200 us),
+// follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
+// shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [20, 1000] us.
+constexpr int kQueueLanes = 2;
 struct Coalescer {
     std::mutex mu;
     std::condition_variable done_cv, arrive_cv;
     std::vector<Tier1Req *> pending;
-    int inside = 0;      // threads inside a Tier-1 gate call on this key
-    bool busy = false;
-    long long batches = 0, gates = 0, largest = 0;
+    int inside = 0;       // threads inside a Tier-1 gate call on this key
+    int in_flight = 0;    // gates taken by running batches
+    int running = 0;      // batches running (<= kQueueLanes)
+    bool collecting = false;   // a leader is waiting for stragglers
+    bool lane_busy[kQueueLanes] = {false, false};
+    double window_us = -1.0;   // adaptive straggler window (set on first use)
+    double wait_avg_us = 0.0;
+    long long batches = 0, gates = 0, largest = 0, overlapped = 0;
 };
 
 struct KeyEntry {
@@ -554,7 +564,7 @@ struct KeyEntry {
     std::vector<TfheAmdContext *> lanes;
     std::mutex mu;
     Coalescer q;
-    TfheAmdContext *qlane = nullptr;   // the coalescing queue's lane (used by one leader at a time)
+    TfheAmdContext *qlane[kQueueLanes] = {nullptr, nullptr};   // the queue's lanes (one leader each at a time)
     double *d_var = nullptr;           // KSK row variances [1024][8][4] on the primary's device
 };
 static std::mutex g_reg_mu;
@@ -606,8 +616,10 @@ static void forget_device_keys(const void *k1, const void *k2) {
         std::lock_guard<std::mutex> lk(e->mu);
         for (auto *l : e->lanes) tfhe_amd_context_destroy(l);
         e->lanes.clear();
-        if (e->qlane) tfhe_amd_context_destroy(e->qlane);
-        e->qlane = nullptr;
+        for (auto *&ql : e->qlane) {
+            if (ql) tfhe_amd_context_destroy(ql);
+            ql = nullptr;
+        }
         if (e->d_var) tfhe_amd_internal_free(tfhe_amd_context_device(e->primary), e->d_var);
         e->d_var = nullptr;
         tfhe_amd_context_destroy(e->primary);
@@ -779,12 +791,11 @@ static int coalesce_window_us() {
     return v;
 }
 
-// Runs one batch of queued gates on lane l: one gate kind -> one host gate batch, several kinds
-// -> one mixed launch (above); inputs are staged before anything is written, so a result may
-// alias any input of its own call; each request gets its key-switch input back, from which its
+// A batch of queued gates holding more than one gate kind runs as ONE mixed launch per 512 gates
+// (tfhe_amd_gate_batch_mixed_host: one blind rotation + one key switch for all kinds; run_tier1_batch
+// below takes the single-kind batches).  Inputs are staged before anything is written, so a result
+// may alias any input of its own call; each request gets its key-switch input back, from which its
 // caller sums current_variance as the single-gate path.
-// A batch holding more than one gate kind runs as ONE mixed launch (tfhe_amd_gate_batch_mixed_host:
-// one blind rotation + one key switch for all kinds) in rounds of 512 gates.
 static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
     std::vector<int32_t> buf, u;
     std::vector<int> gates;
@@ -834,50 +845,39 @@ static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
             run_tier1_mixed(l, batch);
             return;
         }
-    std::vector<Tier1Req *> group;
+    // one gate kind: host gate batches of one unsliced round each, so that each round's
+    // key-switch inputs are still in the lane's scratch for the variance bookkeeping
     std::vector<int32_t> buf, u;
-    std::vector<bool> taken(batch.size(), false);
-    for (size_t i0 = 0; i0 < batch.size(); ++i0) {
-        if (taken[i0]) continue;
-        const int gate = batch[i0]->gate;
-        group.clear();
-        for (size_t i = i0; i < batch.size(); ++i)
-            if (!taken[i] && batch[i]->gate == gate) {
-                taken[i] = true;
-                group.push_back(batch[i]);
-            }
-        const int n = (int)group.size();
-        const bool mux = gate == TFHE_GATE_MUX;
-        const size_t A = (size_t)n * kn;
-        buf.resize(4 * A + 4 * (size_t)n);
-        int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
-        int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
-        for (int i = 0; i < n; ++i) {
-            const Tier1Req *q = group[i];
-            memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
-            memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
-            if (mux) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
+    const int gate = batch[0]->gate, n = (int)batch.size();
+    const bool mux = gate == TFHE_GATE_MUX;
+    const size_t A = (size_t)n * kn;
+    buf.resize(4 * A + 4 * (size_t)n);
+    int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
+    int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
+    for (int i = 0; i < n; ++i) {
+        const Tier1Req *q = batch[i];
+        memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
+        memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
+        if (mux) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
+    }
+    const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
+    for (int s0 = 0; s0 < n; s0 += round) {
+        const int m = std::min(round, n - s0);
+        const size_t o = (size_t)s0 * kn;
+        const int rc = tfhe_amd_gate_batch_host(l, gate, m, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
+                                                mux ? ca + o : nullptr, mux ? cb + s0 : nullptr);
+        if (rc != TFHE_AMD_OK) {
+            for (int i = s0; i < n; ++i) batch[i]->rc = rc;
+            return;
         }
-        // one unsliced round at a time, so that its key-switch inputs are still in the scratch
-        const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
-        for (int s0 = 0; s0 < n; s0 += round) {
-            const int m = std::min(round, n - s0);
-            const size_t o = (size_t)s0 * kn;
-            const int rc = tfhe_amd_gate_batch_host(l, gate, m, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
-                                                    mux ? ca + o : nullptr, mux ? cb + s0 : nullptr);
-            if (rc != TFHE_AMD_OK) {
-                for (int i = s0; i < n; ++i) group[i]->rc = rc;
-                break;
-            }
-            ks_input_of_last(l, m, mux ? 2 : 1, u);
-            for (int i = 0; i < m; ++i) {
-                Tier1Req *q = group[s0 + i];
-                memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
-                q->r->b = rb[s0 + i];
-                // current_variance is summed by each caller after the batch (in parallel, off the
-                // queue's critical path): 8 192 table reads per gate
-                q->u.assign(u.begin() + (size_t)i * kN, u.begin() + (size_t)(i + 1) * kN);
-            }
+        ks_input_of_last(l, m, mux ? 2 : 1, u);
+        for (int i = 0; i < m; ++i) {
+            Tier1Req *q = batch[s0 + i];
+            memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
+            q->r->b = rb[s0 + i];
+            // current_variance is summed by each caller after the batch (in parallel, off the
+            // queue's critical path): 8 192 table reads per gate
+            q->u.assign(u.begin() + (size_t)i * kN, u.begin() + (size_t)(i + 1) * kN);
         }
     }
 }
@@ -898,41 +898,65 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     Coalescer &q = e->q;
     Tier1Req req{gate, r, a, b, c};
     std::unique_lock<std::mutex> lk(q.mu);
+    if (q.window_us < 0) q.window_us = coalesce_window_us();
     q.inside += 1;
     q.pending.push_back(&req);
-    q.arrive_cv.notify_one();
+    q.arrive_cv.notify_all();
     while (!req.done) {
-        if (q.busy) {
+        if (req.taken || q.collecting || q.running >= kQueueLanes || q.pending.empty()) {
             q.done_cv.wait(lk);
             continue;
         }
-        q.busy = true;   // this thread leads the next batch
-        if ((int)q.pending.size() < q.inside && coalesce_window_us() > 0)
-            q.arrive_cv.wait_for(lk, std::chrono::microseconds(coalesce_window_us()),
-                                 [&] { return (int)q.pending.size() >= q.inside; });
+        // this thread leads the next batch, on a free lane
+        int li = 0;
+        while (q.lane_busy[li]) ++li;
+        q.lane_busy[li] = true;
+        q.running += 1;
+        q.collecting = true;
+        // stragglers: every thread inside a call and not in a running batch enqueues first
+        auto all_in = [&] { return (int)q.pending.size() >= q.inside - q.in_flight; };
+        if (!all_in() && q.window_us > 0) {
+            const auto t0 = std::chrono::steady_clock::now();
+            const bool ok = q.arrive_cv.wait_for(lk, std::chrono::duration<double, std::micro>(q.window_us), all_in);
+            if (ok) {
+                const double w = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+                q.wait_avg_us = q.wait_avg_us > 0 ? 0.8 * q.wait_avg_us + 0.2 * w : w;
+                q.window_us = std::min(1000.0, std::max(20.0, 4.0 * q.wait_avg_us + 20.0));
+            } else {
+                q.window_us = std::max(20.0, 0.75 * q.window_us);
+            }
+        }
+        q.collecting = false;
         std::vector<Tier1Req *> batch;
         batch.swap(q.pending);
+        for (Tier1Req *x : batch) x->taken = true;
+        q.in_flight += (int)batch.size();
+        if (q.running > 1) q.overlapped += 1;
+        q.done_cv.notify_all();   // another waiting thread may lead the next batch on the other lane
         lk.unlock();
-        // the queue's own lane (stream + scratch), not the leader thread's: a thread that only
+        // the queue's own lanes (stream + scratch), not the leader thread's: a thread that only
         // ever enqueues needs no lane, and leaders change from batch to batch
         TfheAmdContext *l;
         {
             std::lock_guard<std::mutex> lg(e->mu);
-            if (!e->qlane) e->qlane = tfhe_amd_context_lane(e->primary);
-            l = e->qlane;
+            if (!e->qlane[li]) e->qlane[li] = tfhe_amd_context_lane(e->primary);
+            l = e->qlane[li];
         }
         if (!l) die_dramatically("tfhe_amd: cannot create the Tier-1 queue's GPU lane");
-        run_tier1_batch(l, batch);
+        if (!batch.empty()) run_tier1_batch(l, batch);
         lk.lock();
         for (Tier1Req *x : batch) x->done = true;
+        q.in_flight -= (int)batch.size();
+        q.running -= 1;
+        q.lane_busy[li] = false;
         q.batches += 1;
         q.gates += (long long)batch.size();
         q.largest = std::max(q.largest, (long long)batch.size());
-        q.busy = false;
         q.done_cv.notify_all();
+        q.arrive_cv.notify_all();   // a collecting leader's expected count changed
     }
     q.inside -= 1;
-    q.arrive_cv.notify_one();   // a leader may be waiting for this thread
+    q.arrive_cv.notify_all();   // a leader may be waiting for this thread
     lk.unlock();
     check(req.rc, "gate");
     r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
@@ -944,8 +968,9 @@ EXPORT int tfhe_amd_tier1_prepare(const TFheGateBootstrappingCloudKeySet *bk) {
     if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
     std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
     std::lock_guard<std::mutex> lk(e->mu);
-    if (!e->qlane) e->qlane = tfhe_amd_context_lane(e->primary);
-    return e->qlane ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
+    for (auto *&ql : e->qlane)
+        if (!ql) ql = tfhe_amd_context_lane(e->primary);
+    return e->qlane[0] && e->qlane[1] ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
 }
 
 EXPORT int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches,

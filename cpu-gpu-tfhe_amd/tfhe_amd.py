@@ -397,6 +397,8 @@ class Context:
         one blind-rotation and one key-switch launch."""
         g = np.array([GATES[x] if isinstance(x, str) else int(x) for x in gates], dtype=np.int32)
         ca_a = i32(ca_a); B = ca_a.shape[0]
+        if g.shape != (B,):
+            raise TfheAmdError(f"gates: need one gate kind per row ({B}), got {g.shape[0]}")
         r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
         _check(lib.tfhe_amd_gate_batch_mixed_host(self.h, B, g.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _p(r_a),
                                                   _p(r_b), _p(ca_a), _p(i32(ca_b)), _p(i32(cb_a)), _p(i32(cb_b)),
@@ -578,6 +580,18 @@ class MultiContext:
         """tfhe_amd_multi_circuit_run_dev: shards[i] = (wires_a [n_wires][B_i][500], wires_b [n_wires][B_i])
         on slot i's device.  Enqueued on every slot; call sync()."""
         k = len(self.devices)
+        if len(shards) != k:
+            raise TfheAmdError(f"need {k} shards, got {len(shards)}")
+        for i, sh in enumerate(shards):
+            wa, wb = sh[0], sh[1]
+            if wa.dim() != 3 or wa.shape[2] != n_lwe or tuple(wb.shape) != tuple(wa.shape[:2]):
+                raise TfheAmdError(f"shard {i}: need wires_a [n_wires][B][500] and wires_b [n_wires][B], "
+                                   f"got {tuple(wa.shape)} / {tuple(wb.shape)}")
+            for j, t in enumerate((wa, wb)):
+                if not t.is_cuda or t.dtype != torch.int32 or not t.is_contiguous():
+                    raise TfheAmdError(f"shard {i} tensor {j}: need a contiguous int32 GPU tensor")
+                if t.device.index is not None and t.device.index != self.devices[i]:
+                    raise TfheAmdError(f"shard {i} tensor {j} is on cuda:{t.device.index}, slot device {self.devices[i]}")
         counts = (ctypes.c_int * k)(*[int(sh[0].shape[1]) for sh in shards])
         wa = (_VP * k)(*[sh[0].data_ptr() for sh in shards])
         wb = (_VP * k)(*[sh[1].data_ptr() for sh in shards])
@@ -617,6 +631,7 @@ GATES.update({"MAJ": 11, "XOR3": 12, "NOT": 13, "COPY": 14, "CONST": 15})
 _IP = ctypes.POINTER(ctypes.c_int)
 lib.tfhe_amd_circuit_create.argtypes = [ctypes.POINTER(_VP)]
 lib.tfhe_amd_circuit_destroy.argtypes = [_VP]
+lib.tfhe_amd_circuit_state_count.argtypes = [_VP]
 lib.tfhe_amd_circuit_inputs.argtypes = [_VP, ctypes.c_int]
 lib.tfhe_amd_circuit_gate.argtypes = [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
 lib.tfhe_amd_circuit_lincomb.argtypes = [_VP, ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_int32,
@@ -668,6 +683,10 @@ class Circuit:
             self.close()
         except Exception:
             pass
+
+    def state_count(self):
+        """contexts this circuit holds device state for (dropped when a context is destroyed)"""
+        return self._w(lib.tfhe_amd_circuit_state_count(self.h), "state_count")
 
     def _w(self, rc, what):
         if rc < 0:

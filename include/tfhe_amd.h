@@ -198,13 +198,16 @@ int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const 
  * a thread's lanes are released when it exits (0 if the key has no device context). */
 int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
 
-/* Concurrent Tier-1 gate calls on one key are coalesced: a calling thread enqueues its gate; the
- * first waiting thread that finds no batch running waits until every thread inside a gate call
- * has enqueued (at most TFHE_AMD_TIER1_WINDOW_US, default 200 us), takes every pending gate and
- * runs them as one batch per gate kind on the queue's lane, while later calls queue for the next
- * batch (a lone thread runs its gate at once, B = 1).  Results, aliasing and current_variance are
- * as for a lone call.  env TFHE_AMD_TIER1_COALESCE=0 disables the queue (per-thread lanes, B = 1
- * launches).
+/* Concurrent Tier-1 gate calls on one key are coalesced: a calling thread enqueues its gate; a
+ * waiting thread that finds one of the queue's two lanes free becomes the leader of the next
+ * batch: it waits until every thread inside a gate call and not in a running batch has enqueued
+ * (an adaptive window: TFHE_AMD_TIER1_WINDOW_US, default 200 us, at first, then 4x the observed
+ * wait, within 20 - 1000 us), takes every pending gate and runs them on its lane — one gate kind
+ * as one gate batch, several kinds as one mixed launch (one blind rotation + one key switch) per
+ * 512 gates — while later calls queue for the next batch, which the other lane can stage and
+ * launch while this one is still running (a lone thread runs its gate at once, B = 1).  Results,
+ * aliasing and current_variance are as for a lone call.  env TFHE_AMD_TIER1_COALESCE=0 disables
+ * the queue (per-thread lanes, B = 1 launches).
  * queue_stats: batches run, gates they held, the largest batch (reset = 1 zeroes them). */
 int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long long *batches, long long *gates,
                                long long *largest, int reset);
@@ -276,6 +279,9 @@ int tfhe_amd_fp64_ceiling(int device, int waves_per_simd, double seconds, double
  * Builders return the new wire id (>= 0) or a negative TFHE_AMD_E* code. */
 int tfhe_amd_circuit_create(TfheAmdCircuit **out);
 int tfhe_amd_circuit_destroy(TfheAmdCircuit *c);
+/* number of contexts the circuit holds device state (level tables, scratch) for; a context's
+ * state is dropped when the context is destroyed */
+int tfhe_amd_circuit_state_count(TfheAmdCircuit *c);
 /* `count` fresh input wires; returns the first id */
 int tfhe_amd_circuit_inputs(TfheAmdCircuit *c, int count);
 /* one gate (TFHE_GATE_*); unused inputs ignored (MUX: a ? b : cc; CONST: a = bit value) */

@@ -345,3 +345,31 @@ def test_circuit_oracle_evaluator_decrypts_like_plaintext(keyset, okey):
     for w in range(C.info()["wires"]):
         dec = keyset.decrypt(*W[w])
         assert np.array_equal(dec, np.broadcast_to(ref[w], dec.shape)), w   # CONST wires: a scalar
+
+
+@pytest.mark.gpu
+def test_circuit_state_dropped_with_its_context(keyset, rng):
+    """A circuit keeps device state (level tables, scratch) per executing context; destroying the
+    context drops it (keyed by a never-reused context uid, so a context allocated later at the
+    same address starts clean).  One circuit on 4 successive contexts: at most one state at a
+    time, none after each context is closed, results right every time."""
+    import torch
+    C = T.Circuit()
+    a, b = C.inputs(2)
+    o = C.gate("XOR", a, b)
+    B = 8
+    free0 = None
+    for k in range(4):
+        c = T.Context(keyset.bk, keyset.ksk, device=0)
+        x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+        got = C.run(c, B, {a: x, b: y}, [o], keyset, rng)
+        assert np.array_equal(got[o], x ^ y)
+        assert C.state_count() == 1
+        c.close()
+        assert C.state_count() == 0
+        torch.cuda.synchronize()
+        free = torch.cuda.mem_get_info()[0]
+        if free0 is None:
+            free0 = free
+        assert abs(free - free0) < (64 << 20), "device memory grows with each context"
+    C.close()
