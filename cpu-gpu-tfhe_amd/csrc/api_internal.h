@@ -64,3 +64,6 @@ void tfhe_amd_internal_forget_multi(const void *bkfft);
 // circuit.cpp: drops every circuit's device state (tables, scratch) held for a context; called by
 // tfhe_amd_context_destroy (context uids are never reused, so a later context cannot inherit it)
 void tfhe_amd_internal_circuits_forget_context(unsigned long long ctx_uid);
+// the TFHE API's L1 entry points on host data (engine.cpp): op 0 = tGswFFTExternMulToTLwe (arg = key
+// indices [B]), op 1 = tfhe_blindRotate_FFT (arg = bara [B][iters]); acc [B][2][1024] in place, exact
+int tfhe_amd_internal_l1(TfheAmdContext *c, int op, int B, int iters, const int32_t *arg, int32_t *acc);

@@ -66,7 +66,8 @@ __device__ __forceinline__ void crt4_give(V4Shared &sh, const uint32_t (&O)[2][1
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) mine[(c * 8 + rr) * 64 + L] = O[c][give + rr];
 }
-template <int S>
+// XP (external product only, tGswFFTExternMulToTLwe): the result replaces the accumulator
+template <int S, bool XP = false>
 __device__ __forceinline__ void crt4_take(V4Shared &sh, const uint32_t (&O)[2][16], int L, const V4Args &g) {
     const uint32_t *other = sh.scratch[1 - S];
     constexpr int keep = 8 * S;
@@ -78,11 +79,13 @@ __device__ __forceinline__ void crt4_take(V4Shared &sh, const uint32_t (&O)[2][1
             const uint32_t xm = O[c][keep + rr];
             const uint32_t x0 = S == 0 ? xm : xo, x1 = S == 0 ? xo : xm;
             const int j = L + 64 * (keep + rr);
-            e_store(sh.E[c], j, sh.E[c][j] + crt_lazy(x0, x1, g.crt_h, g.crt_hp));
+            e_store(sh.E[c], j, (XP ? 0u : sh.E[c][j]) + crt_lazy(x0, x1, g.crt_h, g.crt_hp));
         }
 }
 
-// one CMux step for key index i and rotation a (1..2N-1); called by both waves
+// one CMux step for key index i and rotation a (1..2N-1); called by both waves.  XP: the
+// external product alone, ACC <- BK_i (x) ACC (tgsw-fft-operations.cu:124-264; a unused)
+template <bool XP = false>
 __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, int a, int s, int L) {
     const uint32_t q = s ? kQ1 : kQ0;
     uint32_t *sc = sh.scratch[s];
@@ -94,7 +97,8 @@ __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, in
     for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const uint32_t t = sh.E[c][base + 64 * r] - sh.E[c][L + 64 * r] + kDecompOffset;
+            const uint32_t t = (XP ? 0u : sh.E[c][base + 64 * r] - sh.E[c][L + 64 * r]) +
+                               (XP ? sh.E[c][L + 64 * r] : 0u) + kDecompOffset;
             D[2 * c][r] = ((t >> 22) & 1023u) + (q - 512u);
             D[2 * c + 1][r] = ((t >> 12) & 1023u) + (q - 512u);
         }
@@ -139,8 +143,8 @@ __device__ __forceinline__ void cmux_v4(V4Shared &sh, const V4Args &g, int i, in
     if (s == 0) crt4_give<0>(sh, O, L);
     else crt4_give<1>(sh, O, L);
     __syncthreads();
-    if (s == 0) crt4_take<0>(sh, O, L, g);
-    else crt4_take<1>(sh, O, L, g);
+    if (s == 0) crt4_take<0, XP>(sh, O, L, g);
+    else crt4_take<1, XP>(sh, O, L, g);
     __syncthreads();
 }
 
@@ -285,6 +289,21 @@ __global__ __launch_bounds__(kV4Threads, 2) void k_blind_rotate_v4_debug(V4Args 
     for (int j = tid; j < 2 * kN; j += kV4Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];
 }
 
+// tGswFFTExternMulToTLwe batch: accumulator b (acc [B][2][kN]) <- BK_{key_index[b]} (x) acc, exact
+__global__ __launch_bounds__(kV4Threads, 2) void k_external_product_v4(V4Args g, const int32_t *__restrict__ key_index,
+                                                                        int32_t *__restrict__ acc) {
+    __shared__ V4Shared sh;
+    const int tid = threadIdx.x;
+    const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = tid & 63;
+    int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
+    for (int j = tid; j < 2 * kN; j += kV4Threads) e_store(sh.E[j >> kLogN], j & (kN - 1), (uint32_t)accg[j]);
+    const int i = key_index[blockIdx.x];
+    __syncthreads();
+    cmux_v4<true>(sh, g, i, 0, s, L);
+    for (int j = tid; j < 2 * kN; j += kV4Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];
+}
+
 unsigned brv10(unsigned x) {
     unsigned r = 0;
     for (int i = 0; i < kLogN; i++) { r = (r << 1) | (x & 1); x >>= 1; }
@@ -377,6 +396,15 @@ hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, c
     else
         hipLaunchKernelGGL(k_blind_rotate_v4_rows<2>, dim3((unsigned)grid), dim3(kV4Threads), 0, s, v4_args(key), B,
                            total, rows, wa, wb, mu, u_a, u_b, gd);
+    return hipGetLastError();
+}
+
+hipError_t launch_external_product_v4(const DeviceKey &key, int B, const int32_t *key_index, int32_t *acc,
+                                      hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    if (!key.bk_v2) return hipErrorInvalidValue;
+    trace_kernel("k_external_product_v4");
+    hipLaunchKernelGGL(k_external_product_v4, dim3(B), dim3(kV4Threads), 0, s, v4_args(key), key_index, acc);
     return hipGetLastError();
 }
 

@@ -657,6 +657,54 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     return TFHE_AMD_OK;
 }
 
+// tGswFFTExternMulToTLwe (tgsw-fft-operations.cu:124-264) for B accumulators acc [B][2][kN] with
+// key indices key_index [B] (device arrays): acc <- BK_i (x) acc, exact (v4 arithmetic)
+extern "C" int tfhe_amd_external_product_dev(TfheAmdContext *c, int B, const int32_t *key_index, int32_t *acc,
+                                             void *stream) {
+    if (!c || B < 0 || !c->key.has_bk) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    if (!key_index || !acc) return TFHE_AMD_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
+    TraceScope trace(c);
+    HIPCHK(launch_external_product_v4(c->key, B, key_index, acc, s));
+    return TFHE_AMD_OK;
+}
+
+// The L1 entry points of the TFHE API on host data (tfhe_api.cpp): op 0 = external product
+// (arg = key indices [B]), op 1 = tfhe_blindRotate_FFT (arg = bara [B][iters], the exact v4 CMux
+// steps, skipping a_i = 0 as lwe-bootstrapping-functions-fft.cu:705); acc [B][2][kN] in place.
+int tfhe_amd_internal_l1(TfheAmdContext *c, int op, int B, int iters, const int32_t *arg, int32_t *acc) {
+    if (!c || B <= 0 || !arg || !acc || !c->key.has_bk || (op == 1 && (iters < 0 || iters > kn))) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
+    TraceScope trace(c);
+    const size_t na = op == 0 ? (size_t)B : (size_t)B * (size_t)(iters > 0 ? iters : 1);
+    int32_t *d_acc = nullptr, *d_arg = nullptr;
+    HIPCHK(hipMalloc(&d_acc, sizeof(int32_t) * 2 * kN * (size_t)B));
+    if (hipMalloc(&d_arg, sizeof(int32_t) * na) != hipSuccess) {
+        (void)hipFree(d_acc);
+        return TFHE_AMD_E_NOMEM;
+    }
+    hipError_t e = hipMemcpyAsync(d_acc, acc, sizeof(int32_t) * 2 * kN * (size_t)B, hipMemcpyHostToDevice, c->stream);
+    const size_t arg_words = op == 0 ? (size_t)B : (size_t)B * iters;
+    if (e == hipSuccess && arg_words)
+        e = hipMemcpyAsync(d_arg, arg, sizeof(int32_t) * arg_words, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = op == 0 ? launch_external_product_v4(c->key, B, d_arg, d_acc, c->stream)
+                    : launch_blind_rotate_v4_debug(c->key, B, iters, d_acc, d_arg, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(acc, d_acc, sizeof(int32_t) * 2 * kN * (size_t)B, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_acc);
+    (void)hipFree(d_arg);
+    HIPCHK(e);
+    return TFHE_AMD_OK;
+}
+
 // Host batches of more than one blind-rotation round are pipelined in slices of one round:
 // slice s is computed on the context's stream while one copy stream moves slice s + 1 in and
 // another moves slice s - 1 out, and the host stages / unstages the pinned buffers meanwhile.

@@ -134,6 +134,9 @@ hipError_t launch_blind_rotate_v4(const DeviceKey &key, int B, int halves, const
                                   int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v4_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
+// tGswFFTExternMulToTLwe, exact (v4 arithmetic): acc [B][2][kN] <- BK_{key_index[b]} (x) acc
+hipError_t launch_external_product_v4(const DeviceKey &key, int B, const int32_t *key_index, int32_t *acc,
+                                      hipStream_t s);
 // circuit level (v4 kernel): B instances x nrows rows, wires [W][B] ciphertexts, u slots r B + k
 hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,

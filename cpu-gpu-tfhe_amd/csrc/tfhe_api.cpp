@@ -297,7 +297,25 @@ struct BkFFTImpl {
     LweBootstrappingKeyFFT pub;
     std::vector<int32_t> bk_coef;             // [kn][4][2][kN]   (NTT conversion happens on the GPU)
     LweKeySwitchKey *ks;                      // deep copy (owned)
+    // pub.bkFFT: the reference's array of kn TGswSampleFFT (tgsw.h:78-96), so that callers can
+    // pass bk->bkFFT + i to tGswFFTExternMulToTLwe; the samples themselves live on the GPU (null
+    // all_samples) and an element maps back to (this key, i) through g_gsw (below)
+    std::vector<TGswSampleFFT> gsw;
 };
+
+// key of every live TGswSampleFFT array: its first element -> the key (L1 entry points)
+static std::mutex g_gsw_mu;
+static std::map<const TGswSampleFFT *, BkFFTImpl *> g_gsw;
+static BkFFTImpl *gsw_key_of(const TGswSampleFFT *p, int *index) {
+    std::lock_guard<std::mutex> lk(g_gsw_mu);
+    auto it = g_gsw.upper_bound(p);
+    if (it == g_gsw.begin()) return nullptr;
+    --it;
+    const ptrdiff_t i = p - it->first;
+    if (i < 0 || i >= (ptrdiff_t)it->second->gsw.size()) return nullptr;
+    *index = (int)i;
+    return it->second;
+}
 
 static KskImpl *ksk_of(const LweKeySwitchKey *k) { return reinterpret_cast<KskImpl *>(const_cast<LweKeySwitchKey *>(k)); }
 static BkFFTImpl *bkfft_of(const LweBootstrappingKeyFFT *k) {
@@ -390,7 +408,11 @@ LweBootstrappingKeyFFT *tfhe_amd::api::new_bkfft(const LweBootstrappingKey *bk) 
         dst->samples[s].current_variance = bk->ks->ks0_raw[s].current_variance;
     }
     *const_cast<const LweKeySwitchKey **>(&f->pub.ks) = f->ks;
-    *const_cast<const TGswSampleFFT **>(&f->pub.bkFFT) = reinterpret_cast<const TGswSampleFFT *>(f);
+    f->gsw.reserve(kn);
+    for (int i = 0; i < kn; ++i) f->gsw.push_back(TGswSampleFFT{nullptr, nullptr, kK, kL});
+    *const_cast<const TGswSampleFFT **>(&f->pub.bkFFT) = f->gsw.data();
+    std::lock_guard<std::mutex> lk(g_gsw_mu);
+    g_gsw[f->gsw.data()] = f;
     return &f->pub;
 }
 
@@ -399,6 +421,10 @@ static void forget_device_keys(const void *k1, const void *k2);
 static void delete_bkfft(LweBootstrappingKeyFFT *k) {
     if (!k) return;
     BkFFTImpl *f = bkfft_of(k);
+    {
+        std::lock_guard<std::mutex> lk(g_gsw_mu);
+        g_gsw.erase(f->gsw.data());
+    }
     forget_device_keys(k, f->ks);
     tfhe_amd_internal_forget_multi(k);
     delete_ksk(f->ks);
@@ -770,6 +796,110 @@ EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const Lwe
     const double v = ks_variance(ks, sample->a);   // before: result may alias sample
     check(tfhe_amd_keyswitch_batch_host(l, 1, sample->a, &sample->b, result->a, &result->b), "lweKeySwitch");
     result->current_variance = v;
+}
+
+// ------------------------------------------------------------------ L1: blind rotation parts
+// tfhe.h:42-43 (lwe-bootstrapping-functions-fft.cu:676-737, 1408-1456) and tgsw_functions.h:70
+// (tgsw-fft-operations.cu:124-264) on the key's GPU context, exact (the NTT kernel's arithmetic):
+// a caller that holds bk->bkFFT->bkFFT can drive the loop itself, as the reference allows.
+
+struct TorusPolyImpl {
+    TorusPolynomial pub;
+    std::vector<Torus32> c;
+};
+struct TLweSampleImpl {
+    TLweSample pub;
+    std::vector<Torus32> coefs;
+    std::vector<TorusPolynomial> polys;
+};
+// tlwe.h:222, polynomials.h:97 (allocation + construction; coefficients zero)
+EXPORT TorusPolynomial *new_TorusPolynomial(const int N) {
+    if (N <= 0) die_dramatically("new_TorusPolynomial: N must be positive");
+    TorusPolyImpl *p = new TorusPolyImpl{TorusPolynomial{N, nullptr}, std::vector<Torus32>((size_t)N, 0)};
+    p->pub.coefsT = p->c.data();
+    return &p->pub;
+}
+EXPORT void delete_TorusPolynomial(TorusPolynomial *obj) { delete reinterpret_cast<TorusPolyImpl *>(obj); }
+EXPORT TLweSample *new_TLweSample(const TLweParams *params) {
+    const int k = params->k, N = params->N;
+    TLweSampleImpl *t = new TLweSampleImpl{TLweSample{nullptr, nullptr, 0., k}, std::vector<Torus32>((size_t)(k + 1) * N, 0), {}};
+    t->polys.reserve(k + 1);
+    for (int i = 0; i <= k; ++i) t->polys.push_back(TorusPolynomial{N, t->coefs.data() + (size_t)i * N});
+    t->pub.a = t->polys.data();
+    t->pub.b = t->pub.a + k;
+    return &t->pub;
+}
+EXPORT void delete_TLweSample(TLweSample *obj) { delete reinterpret_cast<TLweSampleImpl *>(obj); }
+
+static BkFFTImpl *l1_key(const TGswSampleFFT *gsw, const TGswParams *params, int *index) {
+    BkFFTImpl *f = gsw ? gsw_key_of(gsw, index) : nullptr;
+    if (!f) die_dramatically("tfhe_amd: TGswSampleFFT pointer is not part of a bootstrapping key of this library");
+    if (params && (params->tlwe_params->N != kN || params->tlwe_params->k != kK || params->l != kL))
+        die_dramatically("tfhe_amd: only the default gate-bootstrapping parameter set is supported");
+    return f;
+}
+static void tlwe_to_flat(const TLweSample *s, int32_t *acc) {
+    memcpy(acc, s->a[0].coefsT, sizeof(int32_t) * kN);
+    memcpy(acc + kN, s->b->coefsT, sizeof(int32_t) * kN);
+}
+static void flat_to_tlwe(const int32_t *acc, TLweSample *s) {
+    memcpy(s->a[0].coefsT, acc, sizeof(int32_t) * kN);
+    memcpy(s->b->coefsT, acc + kN, sizeof(int32_t) * kN);
+}
+
+// accum <- gsw (x) accum; current_variance 0 as the reference's tLweFFTClear leaves it
+EXPORT void tGswFFTExternMulToTLwe(TLweSample *accum, const TGswSampleFFT *gsw, const TGswParams *params) {
+    int i = 0;
+    BkFFTImpl *f = l1_key(gsw, params, &i);
+    std::vector<int32_t> acc(2 * kN);
+    tlwe_to_flat(accum, acc.data());
+    check(tfhe_amd_internal_l1(lane_for(&f->pub, nullptr), 0, 1, 0, &i, acc.data()), "tGswFFTExternMulToTLwe");
+    flat_to_tlwe(acc.data(), accum);
+    accum->current_variance = 0.;
+}
+
+// n CMux steps with keys bk[0..n) (bk = an element of a key's array; bara_i == 0 skipped, :705);
+// current_variance unchanged (each tfhe_MuxRotate_FFT adds the accumulator's to a zero one)
+EXPORT void tfhe_blindRotate_FFT(TLweSample *accum, const TGswSampleFFT *bk, const int *bara, const int n,
+                                 const TGswParams *bk_params) {
+    int i0 = 0;
+    BkFFTImpl *f = l1_key(bk, bk_params, &i0);
+    if (n < 0 || i0 + n > kn) die_dramatically("tfhe_blindRotate_FFT: n keys past the end of the key");
+    if (n == 0) return;
+    std::vector<int32_t> acc(2 * kN), a(kn, 0);
+    tlwe_to_flat(accum, acc.data());
+    // keys i0 .. i0 + n - 1: steps before i0 are identity (a = 0)
+    for (int i = 0; i < n; ++i) a[i0 + i] = (int32_t)(((bara[i] % k2N) + k2N) % k2N);
+    check(tfhe_amd_internal_l1(lane_for(&f->pub, nullptr), 1, 1, i0 + n, a.data(), acc.data()),
+          "tfhe_blindRotate_FFT");
+    flat_to_tlwe(acc.data(), accum);
+}
+
+// ACC = (0, X^{2N - barb} v) (v itself for barb = 0), blind rotation, extraction at index 0
+// (lwe.cu:41-56): result has dimension N; its current_variance is left as it was (lwe.cu)
+EXPORT void tfhe_blindRotateAndExtract_FFT(LweSample *result, const TorusPolynomial *v, const TGswSampleFFT *bk,
+                                           const int barb, const int *bara, const int n,
+                                           const TGswParams *bk_params) {
+    int i0 = 0;
+    BkFFTImpl *f = l1_key(bk, bk_params, &i0);
+    if (n < 0 || i0 + n > kn) die_dramatically("tfhe_blindRotateAndExtract_FFT: n keys past the end of the key");
+    std::vector<int32_t> acc(2 * kN, 0), a(kn, 0);
+    const int e = ((k2N - barb) % k2N + k2N) % k2N;   // torusPolynomialMulByXai(2N - barb)
+    for (int j = 0; j < kN; ++j) {                   // acc_b[j] = (X^e v)[j]
+        int src = j - e;
+        uint32_t sign = 0;
+        while (src < 0) { src += kN; sign ^= 1; }
+        const uint32_t x = (uint32_t)v->coefsT[src];
+        acc[kN + j] = (int32_t)(sign ? 0u - x : x);
+    }
+    if (n > 0) {
+        for (int i = 0; i < n; ++i) a[i0 + i] = (int32_t)(((bara[i] % k2N) + k2N) % k2N);
+        check(tfhe_amd_internal_l1(lane_for(&f->pub, nullptr), 1, 1, i0 + n, a.data(), acc.data()),
+              "tfhe_blindRotateAndExtract_FFT");
+    }
+    result->a[0] = acc[0];
+    for (int j = 1; j < kN; ++j) result->a[j] = (int32_t)(0u - (uint32_t)acc[kN - j]);
+    result->b = acc[kN];
 }
 
 // ------------------------------------------------------------------ gates

@@ -13,9 +13,11 @@
  *   LweBootstrappingKey(FFT)                  lwebootstrappingkey.h:10-59
  *   TFheGateBootstrapping{ParameterSet,CloudKeySet,SecretKeySet}
  *                                             tfhe_gate_bootstrapping_structures.h:9-63
- * TGswSampleFFT / TLweSampleFFT stay opaque: this engine keeps the bootstrapping key on the
- * GPU in its own transform layouts (fp64 FFT for the default kernel, exact NTT for v1-v5)
- * instead of the reference's LagrangeHalfC one.
+ *   TGswSampleFFT       tgsw.h:78-96 (so that bk->bkFFT->bkFFT + i indexes the key's array)
+ * TLweSampleFFT stays opaque (all_samples / sample are null): this engine keeps the
+ * bootstrapping key on the GPU in its own transform layouts (fp64 FFT for the default kernel,
+ * exact NTT for the guard's recomputation and the L1 entry points) instead of the reference's
+ * LagrangeHalfC one; a TGswSampleFFT of a key is a handle the L1 functions map back to it.
  *
  * Semantics: synchronous, single-sample, reentrant (safe to call from
  * OpenMP threads as Cipher.cpp:116-120 does); result may alias an input; fatal errors
@@ -100,6 +102,13 @@ struct TGswKey {
 struct TGswSample {
     struct TLweSample *all_sample;
     struct TLweSample **bloc_sample;
+    const int k;
+    const int l;
+};
+
+struct TGswSampleFFT {
+    struct TLweSampleFFT *all_samples;
+    struct TLweSampleFFT **sample;
     const int k;
     const int l;
 };
@@ -207,6 +216,21 @@ EXPORT void tfhe_bootstrap_woKS_FFT(LweSample *result, const LweBootstrappingKey
 EXPORT void tfhe_bootstrap_FFT(LweSample *result, const LweBootstrappingKeyFFT *bk, Torus32 mu,
                                const LweSample *x);
 EXPORT void lweKeySwitch(LweSample *result, const LweKeySwitchKey *ks, const LweSample *sample);
+
+/* L1 (tfhe.h:42-43: lwe-bootstrapping-functions-fft.cu:676-737, 1408-1456; tgsw_functions.h:70:
+ * tgsw-fft-operations.cu:124-264).  bk / gsw: an element of a key's array bk->bkFFT->bkFFT (the
+ * loop uses bk + i for step i < n).  Exact products (the reference's FFT truncates its double
+ * result, fft_processor_fftw.cu:177: see DESIGN.md §2). */
+EXPORT void tfhe_blindRotate_FFT(TLweSample *accum, const TGswSampleFFT *bk, const int *bara, const int n,
+                                 const TGswParams *bk_params);
+EXPORT void tfhe_blindRotateAndExtract_FFT(LweSample *result, const TorusPolynomial *v, const TGswSampleFFT *bk,
+                                           const int barb, const int *bara, const int n, const TGswParams *bk_params);
+EXPORT void tGswFFTExternMulToTLwe(TLweSample *accum, const TGswSampleFFT *gsw, const TGswParams *params);
+/* tlwe.h:222-231, polynomials.h:97-102 */
+EXPORT TLweSample *new_TLweSample(const TLweParams *params);
+EXPORT void delete_TLweSample(TLweSample *obj);
+EXPORT TorusPolynomial *new_TorusPolynomial(const int N);
+EXPORT void delete_TorusPolynomial(TorusPolynomial *obj);
 
 /* ---------------------------------------------------------------- gates */
 /* tfhe_gate_bootstrapping_functions.h:48-89; boot-gates.cu:98-448 */

@@ -125,6 +125,11 @@ int tfhe_amd_keyswitch_batch_host(TfheAmdContext *ctx, int B,
  * accumulators acc [B][2][1024] in place, with rotations bara [B][iters]. */
 int tfhe_amd_blind_rotate_dev(TfheAmdContext *ctx, int B, int iters, int32_t *acc,
                               const int32_t *bara, void *stream);
+/* tGswFFTExternMulToTLwe (tgsw_functions.h:70, tgsw-fft-operations.cu:124-264) on B accumulators:
+ * acc [B][2][1024] <- BK_i (x) acc with i = key_index[b] (device arrays), exact (the NTT kernel's
+ * arithmetic); the reference replaces the accumulator by the product the same way. */
+int tfhe_amd_external_product_dev(TfheAmdContext *ctx, int B, const int32_t *key_index, int32_t *acc,
+                                  void *stream);
 
 /* Timing of the engine's own kernels (HIP events on the stream they run on):
  * enable=1 starts accumulating; read returns the summed ms and launch counts of the

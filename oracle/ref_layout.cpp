@@ -37,6 +37,8 @@ int main() {
     Z(TLweSample); F(TLweSample, a); F(TLweSample, b); F(TLweSample, current_variance); F(TLweSample, k);
     Z(TGswKey); F(TGswKey, params); F(TGswKey, tlwe_params); F(TGswKey, key); F(TGswKey, tlwe_key);
     Z(TGswSample); F(TGswSample, all_sample); F(TGswSample, bloc_sample); F(TGswSample, k); F(TGswSample, l);
+    Z(TGswSampleFFT); F(TGswSampleFFT, all_samples); F(TGswSampleFFT, sample); F(TGswSampleFFT, k);
+    F(TGswSampleFFT, l);
     Z(LweKeySwitchKey); F(LweKeySwitchKey, n); F(LweKeySwitchKey, t); F(LweKeySwitchKey, basebit);
     F(LweKeySwitchKey, base); F(LweKeySwitchKey, out_params); F(LweKeySwitchKey, ks0_raw);
     F(LweKeySwitchKey, ks1_raw); F(LweKeySwitchKey, ks);
