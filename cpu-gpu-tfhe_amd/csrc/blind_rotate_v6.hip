@@ -602,259 +602,6 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
     for (int r = 0; r < 16; ++r) accg[L + 64 * r] = (int32_t)ac[r];
 }
 
-#ifdef TFHE_AMD_EXPERIMENTAL
-// ---------------------------------------------------------------- v8: 4 waves per ciphertext
-// For launches of at most 2 ciphertexts per CU (B <= 512 on 256 CUs), where v6 leaves one wave
-// per SIMD: a 256-thread workgroup per ciphertext, so two ciphertexts per CU fill every SIMD with
-// two waves.  Roles: the owners O0, O1 hold accumulator polynomials 0 and 1 in
-// registers (as v6's two waves); the helpers H0, H1 take the low gadget digits of O0's / O1's
-// polynomial.  Per CMux step:
-//   owner a: rotation in registers (ds_bpermute) -> both digit polynomials; keeps the high one,
-//            hands the low one to helper a (packed int16 through LDS);            barrier S1
-//   all 4:   the forward transform of ONE digit polynomial; its spectrum to LDS;  barrier S2
-//   owner c: MAC of all 4 spectra with BK_i rows 0..3 of output c (the other 3 read from LDS),
-//            inverse transform in its own inverse buffer, rint -> acc_c (guarded as v6)
-// The roles are rotated by two waves on every other workgroup sharing a CU (blocks b and b + CUs),
-// so each SIMD runs one owner and one helper.
-// Measured (profiles/r03_v8_ab, TFHE_AMD_V8=1 vs the default): bit-exact, but slower at every
-// size — B = 512 3.13 vs 2.34 ms (v6p), 256 2.29 vs 1.79, 1 2.28 vs 1.68: after S2 the helpers
-// idle while each owner runs its 4-row MAC and inverse alone (one polynomial, no second stream to
-// interleave), and the two barriers per step serialise the rest.  Kept in EXPERIMENTAL builds.
-constexpr int kV8Threads = 256;
-struct __attribute__((aligned(16))) V8Shared {
-    double2 X[4][kXSlots];     // per wave: forward transposes, then its spectrum (slot [r][L])
-    double2 Xi[2][kXSlots];    // owners' inverse transposes
-    uint32_t lo[2][8 * 64];    // low digits of accumulator polynomial a, int16 pairs [k][L]
-    double2 tw[kT8Words];
-    short bara[512];
-    int barb;
-};
-static_assert(sizeof(V8Shared) <= 80 * 1024, "two v8 workgroups per CU");
-
-// X^a ACC without LDS storage (v6 RREG): lane L takes lane (L - s) mod 64's register r - q of the
-// negacyclic ring of 32 registers; then the signed gadget digits of (X^a - 1) ACC
-__device__ __forceinline__ void v8_digits(const uint32_t (&acc)[16], int a, int L, int32_t (&hi)[16],
-                                          int32_t (&lo)[16]) {
-    const int aa = __builtin_amdgcn_readfirstlane(a) & (k2N - 1);
-    const int s = aa & 63, q = aa >> 6;
-    const int src = ((L - s) & 63) << 2;
-    uint32_t V[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) V[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)acc[r]);
-    if (q & 16) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) V[r] = 0u - V[r];
-    }
-#pragma unroll
-    for (int K = 8; K >= 1; K >>= 1) {
-        if (q & K) {
-            uint32_t t[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) t[r] = r >= K ? V[r - K] : 0u - V[r + 16 - K];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) V[r] = t[r];
-        }
-    }
-    const bool low = L < s;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const uint32_t rot = low ? (r ? V[r - 1] : 0u - V[15]) : V[r];
-        const uint32_t diff = rot - acc[r];
-        hi[r] = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
-        lo[r] = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
-    }
-}
-
-// key row p of output c for this lane's 8 bins (slot 8 L + r)
-__device__ __forceinline__ void v8_load_row(Cx (&b)[8], const double2 *bki, int p, int c) {
-    const double2 *src = bki + (p * 2 + c) * 512;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) b[r] = ld(src + r * 64);
-}
-// Y += D (x) b (complex, per bin)
-__device__ __forceinline__ void v8_mac(Cx (&Y)[8], const Cx (&D)[8], const Cx (&b)[8]) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        Y[r].re = fma_(D[r].re, b[r].re, Y[r].re);
-        Y[r].im = fma_(D[r].re, b[r].im, Y[r].im);
-        Y[r].re = fma_(-D[r].im, b[r].im, Y[r].re);
-        Y[r].im = fma_(D[r].im, b[r].re, Y[r].im);
-    }
-}
-
-__global__ __launch_bounds__(kV8Threads, 2) void k_blind_rotate_v8(V6Args g, int B, int base, BrInput in0, BrInput in1,
-                                                                   int32_t mu, int32_t *__restrict__ u_a,
-                                                                   int32_t *__restrict__ u_b) {
-    __shared__ V8Shared sh;
-    const int gct = base + blockIdx.x;
-    const int half = gct >= B;
-    const int idx = half ? gct - B : gct;
-    const BrInput &in = half ? in1 : in0;
-    const int tid = threadIdx.x;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int L = tid & 63;
-    const int swap = ((int)blockIdx.x / g.cus) & 1;
-    const int role = (wv + 2 * swap) & 3;          // 0, 1: owners of acc 0, 1; 2, 3: helpers of acc 0, 1
-    const int a = role & 1;
-    const bool owner = role < 2;
-    // wave index holding the spectrum of key row p = 2 a' + l (role a' + 2 l)
-    auto wave_of_row = [&](int p) { return (((p >> 1) + 2 * (p & 1)) + 2 * swap) & 3; };
-
-    // gate prologue + modulus switching (lwe-bootstrapping-functions-fft.cu:1851-1858)
-    {
-        const int32_t *xa = in.x_a + (size_t)idx * kn;
-        const int32_t *ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr;
-        for (int i = tid; i < kn; i += kV8Threads) {
-            uint32_t x = (uint32_t)in.sa * (uint32_t)xa[i];
-            if (ya) x += (uint32_t)in.sb * (uint32_t)ya[i];
-            sh.bara[i] = (short)modswitch_2N(x);
-        }
-        if (tid == 0) {
-            uint32_t xb = (uint32_t)in.c + (uint32_t)in.sa * (uint32_t)in.x_b[idx];
-            if (ya) xb += (uint32_t)in.sb * (uint32_t)in.y_b[idx];
-            sh.barb = modswitch_2N(xb);
-        }
-    }
-    for (int e = tid; e < kT8Words; e += kV8Threads) sh.tw[e] = g.tw[t8_src(e)];
-    const Tw4 tA = load_tw_sgpr(g.tw);
-    __syncthreads();
-    uint32_t acc[16];
-    if (owner) {   // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
-        const int e = (k2N - sh.barb) & (k2N - 1);
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            acc[r] = a == 0 ? 0u : (((L + 64 * r - e) & (k2N - 1)) < kN ? (uint32_t)mu : 0u - (uint32_t)mu);
-    }
-    if (g.prio == 8 && owner) __builtin_amdgcn_s_setprio(2);   // owners carry the step's critical path
-    double mx = 0.0;
-    uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;
-    double2 *X = sh.X[wv];
-    int a_next = sh.bara[0];
-    for (int i = 0; i < kn; ++i) {
-        const int rot = a_next;
-        a_next = sh.bara[i + 1 < kn ? i + 1 : i];
-        if (rot == 0) continue;   // identity CMux (:705), uniform over the workgroup
-        const double2 *bki = g.bk + (size_t)i * 8 * 512 + L;
-        Cx x[1][8];
-        if (owner) {
-            int32_t hi[16], lo[16];
-            v8_digits(acc, rot, L, hi, lo);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                x[0][k] = Cx{(double)hi[k], (double)hi[k + 8]};
-                sh.lo[a][k * 64 + L] = ((uint32_t)lo[k] & 0xFFFFu) | ((uint32_t)lo[k + 8] << 16);
-            }
-        }
-        lds_barrier6();                                                // S1
-        if (!owner) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t v = sh.lo[a][k * 64 + L];
-                x[0][k] = Cx{(double)(int32_t)(int16_t)(v & 0xFFFFu), (double)((int32_t)v >> 16)};
-            }
-        }
-        fft_fwd_AB_t<1>(x, X, tA, tw7_fwdB(sh.tw, L), L);
-        const Tw4 tC = tw7_fwdC(sh.tw, L);
-        Cx b0[8], b1[8];
-        if (owner) {   // the first two key rows of output a in flight during pass C
-            v8_load_row(b0, bki, 2 * a, a);
-            v8_load_row(b1, bki, (2 * a + 2) & 3, a);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        fft_fwd_C<1>(x, tC);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) st(X + r * 64 + L, x[0][r]);
-        lds_barrier6();                                                // S2
-        if (!owner) continue;
-        // MAC of output a over rows 2a (own spectrum), 2a + 2 (mod 4), then the two low rows
-        Cx Y[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) Y[r] = Cx{0.0, 0.0};
-        {
-            const double2 *Xp = sh.X[wave_of_row((2 * a + 2) & 3)];
-            Cx D1[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) D1[r] = ld(Xp + r * 64 + L);
-            v8_mac(Y, x[0], b0);
-            v8_load_row(b0, bki, 2 * a + 1, a);
-            v8_mac(Y, D1, b1);
-            v8_load_row(b1, bki, (2 * a + 3) & 3, a);
-        }
-        {
-            const double2 *Xp = sh.X[wave_of_row(2 * a + 1)];
-            const double2 *Xq = sh.X[wave_of_row((2 * a + 3) & 3)];
-            Cx D1[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) { x[0][r] = ld(Xp + r * 64 + L); D1[r] = ld(Xq + r * 64 + L); }
-            SCHED_FENCE();
-            v8_mac(Y, x[0], b0);
-            v8_mac(Y, D1, b1);
-        }
-        // inverse (v6's passes) in this owner's inverse buffer
-        double2 *Xi = sh.Xi[a];
-        pass_dit_C(Y);
-        const Tw4 tB = tw7_invB(sh.tw, L);
-        store_C(Xi, Y, L);
-        wave_sync();
-        load_B_p(Xi, Y, L);
-        SCHED_FENCE();
-        pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
-        {
-            const Tw4 tI = tw7_invA(sh.tw, L);
-            const Cx sg = ld(sh.tw + kT8Sig + L);
-            wave_sync();
-            store_B_ab(Xi, Y, L);
-            wave_sync();
-            load_A(Xi, Y, L);
-            SCHED_FENCE();
-#pragma unroll
-            for (int r = 0; r < 8; r += 2) Y[r] = cmul(Y[r], sg);
-            pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
-            constexpr double kOm[8][2] = {
-                {1.0, 0.0},
-                {0.98078528040323044913, -0.19509032201612826785},
-                {0.92387953251128675613, -0.38268343236508977173},
-                {0.83146961230254523708, -0.55557023301960222474},
-                {0.70710678118654752440, -0.70710678118654752440},
-                {0.55557023301960222474, -0.83146961230254523708},
-                {0.38268343236508977173, -0.92387953251128675613},
-                {0.19509032201612826785, -0.98078528040323044913}};
-#pragma unroll
-            for (int r = 1; r < 8; ++r) Y[r] = cmul(Y[r], Cx{kOm[r][0], kOm[r][1]});
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
-            acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
-        }
-        wave_sync();
-    }
-    if (owner && g.flags) {   // exactness guard, as v6: output a's largest rounding distance
-        if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;
-        const uint32_t h = wave_max_hi(mx);
-        if (L == 0) {
-            g.flags[2 * (size_t)gct + a] = h;
-            atomicMax(g.stats + 1, h);
-        }
-    }
-    __syncthreads();
-    // sample extraction at index 0 (lwe.cu:41-56): a_j = -acc_a[N - j] = E_a[2N - j]
-    int32_t *ua = u_a + (size_t)gct * kN;
-    if (role == 0) {
-        uint32_t *E = reinterpret_cast<uint32_t *>(sh.X[wv]);
-        write_ext(E, acc, L);
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int j = L + 64 * r;
-            ua[j] = (int32_t)E[(k2N - j) & (k2N - 1)];
-        }
-    } else if (role == 1 && L == 0) {
-        u_b[gct] = (int32_t)acc[0];
-    }
-}
-
-#endif  // TFHE_AMD_EXPERIMENTAL
 
 // key conversion: one wave per (i, row, c) polynomial; z_n = b_n + i b_{n + 512} -> FFT / 512
 __global__ __launch_bounds__(64) void k_bk_to_fft(const int32_t *__restrict__ bk_coef, double2 *__restrict__ bkf,
@@ -993,18 +740,6 @@ static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullp
     return g;
 }
 
-// v8 (4 waves per ciphertext) for launches of n ciphertexts: TFHE_AMD_V8=1 forces it for every
-// launch, =0 never; TFHE_AMD_V8_PRIO=8 gives owners issue priority (experiments)
-static bool v8_use(const DeviceKey &key, long n) {
-    (void)key;
-    (void)n;
-#ifdef TFHE_AMD_EXPERIMENTAL
-    static const char *env = getenv("TFHE_AMD_V8");
-    if (env) return atoi(env) != 0;
-#endif
-    return false;
-}
-
 hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                   int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard) {
     if (B <= 0) return hipSuccess;
@@ -1013,16 +748,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        if (v8_use(key, n)) {
-#ifdef TFHE_AMD_EXPERIMENTAL
-            V6Args g = v6_args(key, n, guard);
-            static const char *pe = getenv("TFHE_AMD_V8_PRIO");
-            g.prio = pe ? atoi(pe) : 0;
-            trace_kernel("k_blind_rotate_v8(4-wave)");
-            hipLaunchKernelGGL(k_blind_rotate_v8, dim3((unsigned)n), dim3(kV8Threads), 0, s, g, B, (int)base, in[0],
-                               in1, mu, u_a, u_b);
-#endif
-        } else if (v6_pair(key, n)) {
+        if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
             trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
             hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,

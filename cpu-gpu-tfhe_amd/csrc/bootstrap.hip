@@ -124,73 +124,6 @@ __device__ __forceinline__ void cmux_step(BrShared &sh, const uint32_t *__restri
     __syncthreads();
 }
 
-#ifdef TFHE_AMD_EXPERIMENTAL   // v1 kernels (EXPERIMENTAL=1 builds)
-__global__ __launch_bounds__(kBrThreads) void k_blind_rotate_v1(
-    const uint32_t *__restrict__ bk_ntt, const NttTables *__restrict__ tab, int B,
-    BrInput in0, BrInput in1, int32_t mu, int32_t *__restrict__ u_a, int32_t *__restrict__ u_b) {
-    __shared__ BrShared sh;
-    __shared__ int barb_s;
-    const int tid = threadIdx.x;
-    const int g = blockIdx.x;
-    const int half = g >= B;
-    const int idx = half ? g - B : g;
-    const BrInput &in = half ? in1 : in0;
-
-    // gate prologue + modulus switching (boot-gates.cu:98-397; lwe-bootstrapping-functions-fft.cu:1851-1858)
-    for (int i = tid; i < kn; i += kBrThreads) {
-        uint32_t x = (uint32_t)in.sa * (uint32_t)in.x_a[(size_t)idx * kn + i];
-        if (in.sb) x += (uint32_t)in.sb * (uint32_t)in.y_a[(size_t)idx * kn + i];
-        sh.bara[i] = modswitch_2N(x);
-    }
-    if (tid == 0) {
-        uint32_t xb = (uint32_t)in.c + (uint32_t)in.sa * (uint32_t)in.x_b[idx];
-        if (in.sb) xb += (uint32_t)in.sb * (uint32_t)in.y_b[idx];
-        barb_s = modswitch_2N(xb);
-    }
-    __syncthreads();
-    // ACC = (0, X^{2N - barb} * (mu, ..., mu))   (:1427-1431)
-    {
-        const int e = (k2N - barb_s) & (k2N - 1);
-        for (int j = tid; j < kN; j += kBrThreads) {
-            sh.acc[0][j] = 0;
-            const int si = (j - e) & (k2N - 1);
-            sh.acc[1][j] = si < kN ? (uint32_t)mu : 0u - (uint32_t)mu;
-        }
-    }
-    __syncthreads();
-    const size_t per_i = (size_t)2 * kKpl * 2 * kN;
-    for (int i = 0; i < kn; ++i) {
-        const int a = sh.bara[i];
-        if (a == 0 || a == k2N) continue;   // X^a - 1 == 0: the CMux is the identity
-        cmux_step(sh, bk_ntt + i * per_i, tab, a);
-    }
-    // sample extraction at index 0 (lwe.cu:41-56)
-    int32_t *ua = u_a + (size_t)g * kN;
-    for (int j = tid; j < kN; j += kBrThreads)
-        ua[j] = (int32_t)(j == 0 ? sh.acc[0][0] : 0u - sh.acc[0][kN - j]);
-    if (tid == 0) u_b[g] = (int32_t)sh.acc[1][0];
-}
-
-__global__ __launch_bounds__(kBrThreads) void k_blind_rotate_debug(
-    const uint32_t *__restrict__ bk_ntt, const NttTables *__restrict__ tab, int iters,
-    int32_t *__restrict__ acc, const int32_t *__restrict__ bara) {
-    __shared__ BrShared sh;
-    const int tid = threadIdx.x;
-    const int g = blockIdx.x;
-    int32_t *accg = acc + (size_t)g * 2 * kN;
-    for (int j = tid; j < 2 * kN; j += kBrThreads) sh.acc[j >> kLogN][j & (kN - 1)] = (uint32_t)accg[j];
-    for (int i = tid; i < iters; i += kBrThreads) sh.bara[i] = bara[(size_t)g * iters + i];
-    __syncthreads();
-    const size_t per_i = (size_t)2 * kKpl * 2 * kN;
-    for (int i = 0; i < iters; ++i) {
-        const int a = sh.bara[i];
-        if (a == 0 || a == k2N) continue;
-        cmux_step(sh, bk_ntt + i * per_i, tab, a);
-    }
-    for (int j = tid; j < 2 * kN; j += kBrThreads) accg[j] = (int32_t)sh.acc[j >> kLogN][j & (kN - 1)];
-}
-
-#endif  // TFHE_AMD_EXPERIMENTAL
 
 // coefficient-domain BK -> NTT domain (Montgomery, 1/N folded): one workgroup per polynomial.
 // Output layout [i][s][p][c][kN]  (analogue of init_LweBootstrappingKeyFFT :60-89).
@@ -222,25 +155,5 @@ hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const 
     return hipGetLastError();
 }
 
-#ifdef TFHE_AMD_EXPERIMENTAL   // v1 launchers
-hipError_t launch_blind_rotate(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                               int32_t *u_a, int32_t *u_b, hipStream_t s) {
-    if (B <= 0) return hipSuccess;
-    const BrInput in1 = halves > 1 ? in[1] : in[0];
-    hipLaunchKernelGGL(k_blind_rotate_v1, dim3(B * halves), dim3(kBrThreads), 0, s,
-                       key.bk_ntt, key.tables, B, in[0], in1, mu, u_a, u_b);
-    return hipGetLastError();
-}
-
-hipError_t launch_blind_rotate_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                     const int32_t *bara, hipStream_t s) {
-    if (B <= 0) return hipSuccess;
-    if (iters < 0 || iters > kn) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_blind_rotate_debug, dim3(B), dim3(kBrThreads), 0, s,
-                       key.bk_ntt, key.tables, iters, acc, bara);
-    return hipGetLastError();
-}
-
-#endif  // TFHE_AMD_EXPERIMENTAL
 
 }  // namespace tfhe_amd

@@ -89,16 +89,11 @@ void trace_kernel(const char *name) {
 
 static std::atomic<int> g_br_version{-1};
 
-// Product builds carry the default fp64 kernel (v6) and the exact NTT kernel (v4: the guard's
-// fallback and the exact reference generation); EXPERIMENTAL=1 builds add the earlier and
-// experimental generations (v1 LDS radix-2, v2, v3, v5 latency, v7 shared-key) for A/B work.
-static bool br_available(int v) {
-#ifdef TFHE_AMD_EXPERIMENTAL
-    return v >= 0 && v <= 7;
-#else
-    return v == 0 || v == 4 || v == 6;
-#endif
-}
+// The library carries the default fp64 kernel (v6) and the exact NTT kernel (v4: the guard's
+// fallback, the L1 entry points and the exact reference generation); the earlier and experimental
+// generations (v1 LDS radix-2, v2, v3, v5 latency, v7 shared-key, v8 four-wave) were retired in
+// round 4 (their measurements: DESIGN.md, profiles/README.md).
+static bool br_available(int v) { return v == 0 || v == 4 || v == 6; }
 
 int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
@@ -130,13 +125,6 @@ static hipError_t run_v6_guarded(const DeviceKey &key, int B, int halves, const 
 static hipError_t run_br(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu, int32_t *u_a,
                          int32_t *u_b, hipStream_t s, const Guard *guard) {
     switch (br_version()) {
-#ifdef TFHE_AMD_EXPERIMENTAL
-    case 1: return launch_blind_rotate(key, B, halves, in, mu, u_a, u_b, s);
-    case 2: return launch_blind_rotate_v2(key, B, halves, in, mu, u_a, u_b, s);
-    case 3: return launch_blind_rotate_v3(key, B, halves, in, mu, u_a, u_b, s);
-    case 5: return launch_blind_rotate_v5(key, B, halves, in, mu, u_a, u_b, s);
-    case 7: return launch_blind_rotate_v7(key, B, halves, in, mu, u_a, u_b, s);
-#endif
     case 4: return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s);
     default: return run_v6_guarded(key, B, halves, in, mu, u_a, u_b, s, guard);   // 0, 6
     }
@@ -147,10 +135,6 @@ hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, cons
                                     const Guard *guard) {
     switch (br_version()) {
     case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
-#ifdef TFHE_AMD_EXPERIMENTAL
-    case 5: return launch_blind_rotate_v5_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
-    case 7: return launch_blind_rotate_v7_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
-#endif
     default: {
         hipError_t e = launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
         if (e != hipSuccess || !guard || !guard->flags) return e;
@@ -329,13 +313,11 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         HIPCHK(launch_bk_to_fft(d_coef, c->key.bk_fft, c->key.tw6, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(d_coef));
-#ifndef TFHE_AMD_EXPERIMENTAL
-        // product builds: the v1-layout NTT key and the NTT tables only fed the v4 repack
+        // the v1-layout NTT key and the NTT tables only fed the v4 repack
         HIPCHK(hipFree(c->key.bk_ntt));
         c->key.bk_ntt = nullptr;
         HIPCHK(hipFree(c->key.tables));
         c->key.tables = nullptr;
-#endif
         c->key.has_bk = true;
     }
     if (ksk) {
@@ -395,6 +377,95 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     if (!c->shared_key) free_key(c->key);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+    return TFHE_AMD_OK;
+}
+
+// The device buffers of a context's key, in a fixed order: (pointer, bytes) for each domain the
+// context holds (replicas, digests)
+static std::vector<std::pair<void **, size_t>> key_buffers(DeviceKey &k) {
+    const size_t coef = (size_t)kn * kKpl * 2 * kN;
+    return {{(void **)&k.bk_ntt, k.bk_ntt ? sizeof(uint32_t) * 2 * coef : 0},
+            {(void **)&k.bk_v2, k.bk_v2 ? sizeof(uint32_t) * 2 * coef : 0},
+            {(void **)&k.bk_fft, k.bk_fft ? sizeof(double2) * coef / 2 : 0},
+            {(void **)&k.tw2, k.tw2 ? sizeof(uint2) * kTw2Words : 0},
+            {(void **)&k.tw4, k.tw4 ? sizeof(uint2) * kTw4Words : 0},
+            {(void **)&k.tw6, k.tw6 ? sizeof(double2) * kTw6Words : 0},
+            {(void **)&k.ksk, k.ksk ? sizeof(int32_t) * kN * kKsT * 3 * kKsRow : 0},
+            {(void **)&k.ksk4, k.ksk4 ? sizeof(int32_t) * ksk_v4_words() : 0},
+            {(void **)&k.ksk5, k.ksk5 ? sizeof(int32_t) * ksk_v5_words() : 0},
+            {(void **)&k.tables, k.tables ? sizeof(NttTables) : 0}};
+}
+
+// A context on `device` holding a copy of src's converted device key, copied device to device
+// (key replicas device 0 -> peers): hipMemcpyPeerAsync runs over xGMI when the two
+// GPUs have peer access (enabled here when the driver offers it) and is staged by HIP otherwise;
+// ~180 MB per key instead of the host upload + on-device conversion of every replica.
+extern "C" int tfhe_amd_context_create_replica(TfheAmdContext *src, int device, TfheAmdContext **out) {
+    if (!src || !out) return TFHE_AMD_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return TFHE_AMD_E_ARG;
+    TfheAmdContext *c = new TfheAmdContext();
+    c->device = device;
+    auto fail = [&](int rc) {
+        tfhe_amd_context_destroy(c);
+        return rc;
+    };
+    DeviceScope dev_scope(device);
+    if (dev_scope.rc != hipSuccess) return fail(TFHE_AMD_E_HIP);
+    if (device != src->device) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, device, src->device) == hipSuccess && can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(src->device, 0);
+            if (e != hipSuccess) (void)hipGetLastError();   // already enabled: fine; otherwise HIP stages
+        }
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->gstats, sizeof(uint32_t) * 4) != hipSuccess ||
+        hipMemset(c->gstats, 0, sizeof(uint32_t) * 4) != hipSuccess)
+        return fail(TFHE_AMD_E_HIP);
+    std::lock_guard<std::recursive_mutex> lk(src->mu);
+    {
+        DeviceScope src_scope(src->device);   // src's pending work (conversions) has finished
+        if (hipStreamSynchronize(src->stream) != hipSuccess) return fail(TFHE_AMD_E_HIP);
+    }
+    DeviceKey &k = c->key;
+    k = src->key;            // scalars (CRT constants, has_bk); pointers replaced below
+    k.device = device;
+    auto sb = key_buffers(src->key);
+    auto db = key_buffers(k);
+    for (size_t i = 0; i < db.size(); ++i) *db[i].first = nullptr;
+    for (size_t i = 0; i < db.size(); ++i) {
+        if (!sb[i].second) continue;
+        if (hipMalloc(db[i].first, sb[i].second) != hipSuccess) return fail(TFHE_AMD_E_NOMEM);
+        if (hipMemcpyPeerAsync(*db[i].first, device, *sb[i].first, src->device, sb[i].second, c->stream) != hipSuccess)
+            return fail(TFHE_AMD_E_HIP);
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(TFHE_AMD_E_HIP);
+    const int rc = tfhe_amd_reserve(c, 64);
+    if (rc != TFHE_AMD_OK) return fail(rc);
+    *out = c;
+    return TFHE_AMD_OK;
+}
+
+// FNV-1a 64 over the context's device key buffers (key_buffers order), read back to the host:
+// tests compare a replica's bytes with its source's
+extern "C" int tfhe_amd_context_key_digest(TfheAmdContext *c, unsigned long long *digest) {
+    if (!c || !digest) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint64_t h = 1469598103934665603ull;
+    std::vector<unsigned char> buf;
+    for (auto &b : key_buffers(c->key)) {
+        h = (h ^ (uint64_t)b.second) * 1099511628211ull;   // which domains are present, and their sizes
+        if (!b.second) continue;
+        buf.resize(b.second);
+        HIPCHK(hipMemcpy(buf.data(), *b.first, b.second, hipMemcpyDeviceToHost));
+        for (unsigned char x : buf) h = (h ^ x) * 1099511628211ull;
+    }
+    *digest = h;
     return TFHE_AMD_OK;
 }
 
@@ -643,17 +714,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     TraceScope trace(c);
     ProfScope ps(c, s, true);
     const int v = br_version();
-#ifdef TFHE_AMD_EXPERIMENTAL
-    HIPCHK(v == 1   ? launch_blind_rotate_debug(c->key, B, iters, acc, bara, s)
-           : v == 2 ? launch_blind_rotate_v2_debug(c->key, B, iters, acc, bara, s)
-           : v == 3 ? launch_blind_rotate_v3_debug(c->key, B, iters, acc, bara, s)
-           : (v == 4 || v == 5) ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)   // v5 shares v4's math
-           : v == 7 ? launch_blind_rotate_v7_debug(c->key, B, iters, acc, bara, s)
-                    : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
-#else
     HIPCHK(v == 4 ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)
                   : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
-#endif
     return TFHE_AMD_OK;
 }
 

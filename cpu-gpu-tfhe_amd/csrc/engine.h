@@ -111,22 +111,9 @@ hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const 
                             hipStream_t s);
 // Blind rotation + sample extraction for `halves` x B ciphertexts: ciphertext g of half h
 // reads in[h] at index g and writes u[h*B + g] (u_a row stride kN).
-hipError_t launch_blind_rotate(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                               int32_t *u_a, int32_t *u_b, hipStream_t s);
-// Debug: `iters` CMux steps on explicit accumulators acc [B][2][kN] with bara [B][iters].
-hipError_t launch_blind_rotate_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                     const int32_t *bara, hipStream_t s);
 // v2 (register-resident NTT) variants, blind_rotate.hip
 void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f, uint2 *ts_i);
 hipError_t launch_bk_v1_to_v2(const uint32_t *d_v1, uint32_t *d_v2, hipStream_t s);
-hipError_t launch_blind_rotate_v2(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
-hipError_t launch_blind_rotate_v2_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                        const int32_t *bara, hipStream_t s);
-hipError_t launch_blind_rotate_v3(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
-hipError_t launch_blind_rotate_v3_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                        const int32_t *bara, hipStream_t s);
 // v4 (v2 layout, inverse CT + lazy CRT + periodic accumulator), blind_rotate_v4.hip
 void build_v4_twiddles(const NttTables &t, uint2 *tu_i, uint2 *ts_i, uint2 *tpost);
 // guard != null: guard mode (recompute only the ciphertexts whose v6 flag reached the threshold)
@@ -141,11 +128,6 @@ hipError_t launch_external_product_v4(const DeviceKey &key, int B, const int32_t
 hipError_t launch_blind_rotate_v4_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
                                        const Guard *guard = nullptr);
-// v5 (latency: 8 waves per ciphertext), blind_rotate_v5.hip; same results as v4
-hipError_t launch_blind_rotate_v5(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
-hipError_t launch_blind_rotate_v5_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
 // v6 (fp64 FFT external product, the reference's arithmetic), blind_rotate_v6.hip
 void build_v6_twiddles(double2 *tw);
 hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s);
@@ -156,14 +138,6 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
                                        const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                        const int32_t *bara, hipStream_t s);
-// v7 (v6 arithmetic; BK_i staged in LDS by LDS-DMA and shared by the workgroup's ciphertexts),
-// blind_rotate_v7.hip; same results as v6
-hipError_t launch_blind_rotate_v7(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s);
-hipError_t launch_blind_rotate_v7_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s);
-hipError_t launch_blind_rotate_v7_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
 // which blind-rotation kernel runs: 0 = default (v6), 1..7 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();

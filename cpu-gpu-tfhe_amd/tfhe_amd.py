@@ -70,6 +70,9 @@ def _load():
     L.tfhe_amd_bootstrap_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_I32P] * 4
     L.tfhe_amd_keyswitch_batch_host.argtypes = [_VP, ctypes.c_int] + [_I32P] * 4
     L.tfhe_amd_blind_rotate_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP]
+    L.tfhe_amd_external_product_dev.argtypes = [_VP, ctypes.c_int, _VP, _VP, _VP]
+    L.tfhe_amd_context_create_replica.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(_VP)]
+    L.tfhe_amd_context_key_digest.argtypes = [_VP, ctypes.POINTER(ctypes.c_ulonglong)]
     L.tfhe_amd_profile_enable.argtypes = [_VP, ctypes.c_int]
     L.tfhe_amd_profile_read.argtypes = [_VP, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
@@ -350,6 +353,21 @@ class Context:
         self.h = h.value
         self.device = device
 
+    @classmethod
+    def replica_of(cls, src, device):
+        """tfhe_amd_context_create_replica: src's converted device key copied device to device"""
+        h = _VP()
+        _check(lib.tfhe_amd_context_create_replica(src.h, int(device), ctypes.byref(h)), "context_create_replica")
+        c = cls.__new__(cls)
+        c.bk, c.ksk, c.h, c.device = src.bk, src.ksk, h.value, device
+        return c
+
+    def key_digest(self):
+        """FNV-1a 64 of the context's device key bytes (tfhe_amd_context_key_digest)"""
+        d = ctypes.c_ulonglong()
+        _check(lib.tfhe_amd_context_key_digest(self.h, ctypes.byref(d)), "context_key_digest")
+        return d.value
+
     def close(self):
         if getattr(self, "h", None):
             lib.tfhe_amd_context_destroy(self.h)
@@ -597,6 +615,13 @@ class MultiContext:
         wb = (_VP * k)(*[sh[1].data_ptr() for sh in shards])
         st = None if streams is None else (_VP * k)(*streams)
         _check(lib.tfhe_amd_multi_circuit_run_dev(self.h, circ.h, counts, wa, wb, st), "multi_circuit_run_dev")
+
+    def key_digest(self, i):
+        """FNV-1a 64 of slot i's device key bytes (slots > 0 are peer-copied replicas of slot 0)"""
+        d = ctypes.c_ulonglong()
+        _check(lib.tfhe_amd_context_key_digest(lib.tfhe_amd_multi_context(self.h, int(i)), ctypes.byref(d)),
+               "context_key_digest")
+        return d.value
 
     def guard_stats(self, reset=False):
         """per device slot: (largest rounding distance, ciphertexts recomputed exactly)"""

@@ -63,6 +63,12 @@ int tfhe_amd_context_create(const TFheGateBootstrappingCloudKeySet *bk, int devi
 /* same from raw arrays: bk int32 [500][4][2][1024], ksk int32 [1024][8][4][501] */
 int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk, int device, TfheAmdContext **out);
 int tfhe_amd_context_destroy(TfheAmdContext *ctx);
+/* A context on `device` holding a copy of src's converted device key, copied device to device
+ * (hipMemcpyPeerAsync: xGMI when the GPUs have peer access, staged by HIP otherwise) instead of a
+ * host upload and on-device conversion; the multi-device context builds its slots > 0 this way. */
+int tfhe_amd_context_create_replica(TfheAmdContext *src, int device, TfheAmdContext **out);
+/* FNV-1a 64 of the context's device key bytes (every domain it holds, in a fixed order) */
+int tfhe_amd_context_key_digest(TfheAmdContext *ctx, unsigned long long *digest);
 int tfhe_amd_context_device(const TfheAmdContext *ctx);
 /* device bytes of the context's key material (the transform-domain bootstrapping keys and the
  * key-switching key layouts its kernels read) */

@@ -101,9 +101,9 @@ def test_keyswitch_random_inputs(ctx, okey, rng):
 
 
 def test_kernel_generations_agree(ctx, keyset, rng):
-    """Every blind-rotation generation the build carries (product: v4 exact NTT and v6 fp64
-    FFT, whose rounded products equal the exact ones; EXPERIMENTAL=1 builds also v1, v2, v3, v5,
-    v7) gives identical Torus32 results on the same gates and on explicit CMux steps."""
+    """Both blind-rotation generations the library carries (v4 exact NTT and v6 fp64 FFT, whose
+    rounded products equal the exact ones) give identical Torus32 results on the same gates and
+    on explicit CMux steps."""
     torch = _torch()
     B, iters = 8, 6
     x = rng.integers(0, 2, B)

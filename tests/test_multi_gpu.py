@@ -43,23 +43,71 @@ def test_multi_context_split_bit_exact(ctx, okey, keyset, rng):
         mux = m.gate_host("MUX", sa, sb, ua, ub, va, vb)
         assert np.array_equal(keyset.decrypt(*mux), np.where(s == 1, u, v))
         assert all(r == 0 for _, r in m.guard_stats())
+        # slots 1, 2 hold device-to-device replicas of slot 0's converted key
+        assert len({m.key_digest(i) for i in range(3)}) == 1
     finally:
         m.close()
 
 
-def test_multi_context_all_visible_devices(keyset, rng):
+def _shard_seams(B, world):
+    idx = set()
+    for r in range(world):
+        lo, hi = T.shard_range(B, r, world)
+        idx.update(v for v in (lo, lo + 1, hi - 2, hi - 1) if lo <= v < hi)
+    return np.array(sorted(idx))
+
+
+def test_multi_context_all_visible_devices(keyset, okey, rng):
+    """One slot per visible GPU (slots > 0 hold peer-copied key replicas): every shard's seams
+    Torus32-for-Torus32 against the exact oracle, every output against the truth table, and the
+    whole batch word for word against one context on device 0."""
     torch = _torch()
     n = torch.cuda.device_count()
     if n < 2:
-        pytest.skip("one GPU visible: the split is covered by test_multi_context_split_bit_exact")
+        pytest.skip("one GPU visible: the split is covered by test_multi_context_split_bit_exact "
+                    "(3 slots of device 0) and test_key_replica_bytes_and_results")
     m = T.MultiContext(keyset.bk, keyset.ksk, list(range(n)))
+    one = T.Context(keyset.bk, keyset.ksk, device=0)
     try:
         B = 64 * n + 3
         x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
-        got = m.gate_host("NAND", *(keyset.encrypt(x, rng) + keyset.encrypt(y, rng)))
+        host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+        got = m.gate_host("NAND", *host)
         assert np.array_equal(keyset.decrypt(*got), 1 - (x & y))
+        idx = _shard_seams(B, n)
+        o = okey.gate_batch("NAND", *(v[idx] for v in host))
+        bad = [int(i) for k, i in enumerate(idx) if not (np.array_equal(got[0][i], o[0][k]) and got[1][i] == o[1][k])]
+        assert not bad, f"outputs differing from the oracle (Torus32) at {bad}"
+        ref = one.gate_host("NAND", *host)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+        assert len({m.key_digest(i) for i in range(n)}) == 1, "key replicas differ from slot 0's key"
     finally:
+        one.close()
         m.close()
+
+
+def test_key_replica_bytes_and_results(ctx, okey, keyset, rng):
+    """tfhe_amd_context_create_replica copies a context's converted key device to device (xGMI
+    peer copies between GPUs; here the last visible GPU, device 0 itself on a one-GPU box): the
+    replica's key bytes equal the source's (digest of every domain) and its gates equal the
+    source's word for word and the oracle's at the ends."""
+    torch = _torch()
+    dev = torch.cuda.device_count() - 1
+    r = T.Context.replica_of(ctx, dev)
+    try:
+        assert r.key_digest() == ctx.key_digest()
+        assert r.key_bytes() == ctx.key_bytes()
+        B = 67
+        x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+        host = keyset.encrypt(x, rng) + keyset.encrypt(y, rng)
+        a = r.gate_host("XNOR", *host)
+        b = ctx.gate_host("XNOR", *host)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        idx = np.array([0, B - 1])
+        o = okey.gate_batch("XNOR", *(v[idx] for v in host))
+        assert np.array_equal(a[0][idx], o[0]) and np.array_equal(a[1][idx], o[1])
+    finally:
+        r.close()
 
 
 def test_library_calls_keep_the_callers_current_device(keyset, rng):

@@ -97,6 +97,12 @@ extern "C" int tfhe_amd_context_create_raw(const int32_t *bk, const int32_t *ksk
     busy_wait_us(300);   // key upload + conversion
     return new_context(device, false, out);
 }
+extern "C" int tfhe_amd_context_create_replica(TfheAmdContext *src, int device, TfheAmdContext **out) {
+    if (!src || !out) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(src->mu);
+    busy_wait_us(100);   // peer copies of the converted key
+    return new_context(device, false, out);
+}
 TfheAmdContext *tfhe_amd_context_lane(TfheAmdContext *primary) {
     TfheAmdContext *c = nullptr;
     return new_context(primary->device, true, &c) == TFHE_AMD_OK ? c : nullptr;
@@ -223,6 +229,16 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     if ((size_t)halves * B > (size_t)c->last_rows) return TFHE_AMD_E_ARG;
     memcpy(u_a, c->last_u.data(), sizeof(int32_t) * (size_t)halves * B * kN);
+    return TFHE_AMD_OK;
+}
+int tfhe_amd_internal_l1(TfheAmdContext *c, int op, int B, int iters, const int32_t *arg, int32_t *acc) {
+    if (!c || B <= 0 || !arg || !acc) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    for (int b = 0; b < B; ++b)
+        for (int j = 0; j < 2 * kN; ++j)
+            acc[(size_t)b * 2 * kN + j] = (int32_t)mix((uint32_t)acc[(size_t)b * 2 * kN + j],
+                                                       (uint32_t)(op == 0 ? arg[b] : iters));
+    busy_wait_us(100);
     return TFHE_AMD_OK;
 }
 int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev) {
