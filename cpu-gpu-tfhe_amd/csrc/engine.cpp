@@ -93,7 +93,7 @@ static std::atomic<int> g_br_version{-1};
 // fallback, the L1 entry points and the exact reference generation); the earlier and experimental
 // generations (v1 LDS radix-2, v2, v3, v5 latency, v7 shared-key, v8 four-wave) were retired in
 // round 4 (their measurements: DESIGN.md, profiles/README.md).
-static bool br_available(int v) { return v == 0 || v == 4 || v == 6 || v == 9; }
+static bool br_available(int v) { return v == 0 || v == 4 || v == 6; }
 
 int br_version() {
     int v = g_br_version.load(std::memory_order_relaxed);
@@ -114,34 +114,10 @@ int br_version() {
 static std::atomic<uint32_t> g_guard_hi{0x3FC00000u};
 uint32_t guard_threshold_hi() { return g_guard_hi.load(std::memory_order_relaxed); }
 
-// Which fp64 kernel a launch of n ciphertexts takes: v9 (4 waves per ciphertext) when it has at
-// most 2 ciphertexts per CU, where v6's 2 waves leave one wave per SIMD or idle SIMDs; v6 above.
-// TFHE_AMD_V9=0 never uses v9, =2 always (A/B), TFHE_AMD_BR=9 as 2.
-static int cu_count(int device) {
-    static std::atomic<int> cus[64];
-    const int d = device >= 0 && device < 64 ? device : 0;
-    int n = cus[d].load(std::memory_order_relaxed);
-    if (!n) {
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
-        cus[d].store(n, std::memory_order_relaxed);
-    }
-    return n;
-}
-static bool use_v9(const DeviceKey &key, long n) {
-    static const int mode = [] {
-        const char *e = getenv("TFHE_AMD_V9");
-        return e ? atoi(e) : 0;
-    }();
-    if (!key.bk9) return false;
-    if (mode == 2 || br_version() == 9) return true;
-    return mode == 1 && n <= 2L * cu_count(key.device);
-}
-
 // the default fp64 kernel, then the exact kernel in guard mode over the flags it wrote
 static hipError_t run_v6_guarded(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard) {
-    hipError_t e = use_v9(key, (long)B * halves) ? launch_blind_rotate_v9(key, B, halves, in, mu, u_a, u_b, s, guard)
-                                                 : launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s, guard);
+    hipError_t e = launch_blind_rotate_v6(key, B, halves, in, mu, u_a, u_b, s, guard);
     if (e != hipSuccess || !guard || !guard->flags) return e;
     return launch_blind_rotate_v4(key, B, halves, in, mu, u_a, u_b, s, guard);
 }
@@ -160,9 +136,7 @@ hipError_t launch_blind_rotate_rows(const DeviceKey &key, int B, int nrows, cons
     switch (br_version()) {
     case 4: return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s);
     default: {
-        hipError_t e = use_v9(key, (long)B * nrows)
-                           ? launch_blind_rotate_v9_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard)
-                           : launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
+        hipError_t e = launch_blind_rotate_v6_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
         if (e != hipSuccess || !guard || !guard->flags) return e;
         return launch_blind_rotate_v4_rows(key, B, nrows, rows, wa, wb, mu, u_a, u_b, s, guard);
     }
@@ -244,8 +218,6 @@ static int free_key(DeviceKey &k) {
     if (k.bk_v2) (void)hipFree(k.bk_v2);
     if (k.bk_fft) (void)hipFree(k.bk_fft);
     if (k.tw6) (void)hipFree(k.tw6);
-    if (k.tw9) (void)hipFree(k.tw9);
-    if (k.bk9) (void)hipFree(k.bk9);
     if (k.tw2) (void)hipFree(k.tw2);
     if (k.tw4) (void)hipFree(k.tw4);
     if (k.ksk) (void)hipFree(k.ksk);
@@ -325,10 +297,6 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         build_v6_twiddles(tw6.data());
         HIPCHK(hipMalloc(&c->key.tw6, sizeof(double2) * tw6.size()));
         HIPCHK(hipMemcpy(c->key.tw6, tw6.data(), sizeof(double2) * tw6.size(), hipMemcpyHostToDevice));
-        std::vector<double2> tw9(kTw9Words);
-        build_v9_twiddles(tw9.data());
-        HIPCHK(hipMalloc(&c->key.tw9, sizeof(double2) * tw9.size()));
-        HIPCHK(hipMemcpy(c->key.tw9, tw9.data(), sizeof(double2) * tw9.size(), hipMemcpyHostToDevice));
     }
     delete ht;
 
@@ -343,8 +311,6 @@ static int context_init(TfheAmdContext *c, const int32_t *bk, const int32_t *ksk
         HIPCHK(launch_bk_v1_to_v2(c->key.bk_ntt, c->key.bk_v2, c->stream));
         HIPCHK(hipMalloc(&c->key.bk_fft, sizeof(double2) * (size_t)kn * kKpl * 2 * 512));
         HIPCHK(launch_bk_to_fft(d_coef, c->key.bk_fft, c->key.tw6, c->stream));
-        HIPCHK(hipMalloc(&c->key.bk9, sizeof(double2) * (size_t)kn * kKpl * 2 * 512));
-        HIPCHK(launch_bk_fft_to_v9(c->key.bk_fft, c->key.bk9, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(d_coef));
         // the v1-layout NTT key and the NTT tables only fed the v4 repack
@@ -424,8 +390,6 @@ static std::vector<std::pair<void **, size_t>> key_buffers(DeviceKey &k) {
             {(void **)&k.tw2, k.tw2 ? sizeof(uint2) * kTw2Words : 0},
             {(void **)&k.tw4, k.tw4 ? sizeof(uint2) * kTw4Words : 0},
             {(void **)&k.tw6, k.tw6 ? sizeof(double2) * kTw6Words : 0},
-            {(void **)&k.bk9, k.bk9 ? sizeof(double2) * coef / 2 : 0},
-            {(void **)&k.tw9, k.tw9 ? sizeof(double2) * kTw9Words : 0},
             {(void **)&k.ksk, k.ksk ? sizeof(int32_t) * kN * kKsT * 3 * kKsRow : 0},
             {(void **)&k.ksk4, k.ksk4 ? sizeof(int32_t) * ksk_v4_words() : 0},
             {(void **)&k.ksk5, k.ksk5 ? sizeof(int32_t) * ksk_v5_words() : 0},
@@ -519,8 +483,6 @@ extern "C" long long tfhe_amd_context_key_bytes(const TfheAmdContext *c) {
     if (k.tw2) n += (long long)kTw2Words * 8;
     if (k.tw4) n += (long long)kTw4Words * 8;
     if (k.tw6) n += (long long)kTw6Words * 16;
-    if (k.bk9) n += bk / 2 * 16;
-    if (k.tw9) n += (long long)kTw9Words * 16;
     if (k.ksk) n += (long long)kN * kKsT * 3 * kKsRow * 4;
     if (k.ksk4) n += (long long)ksk_v4_words() * 4;
     if (k.ksk5) n += (long long)ksk_v5_words() * 4;
@@ -752,9 +714,8 @@ extern "C" int tfhe_amd_blind_rotate_dev(TfheAmdContext *c, int B, int iters, in
     TraceScope trace(c);
     ProfScope ps(c, s, true);
     const int v = br_version();
-    HIPCHK(v == 4   ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)
-           : v == 9 ? launch_blind_rotate_v9_debug(c->key, B, iters, acc, bara, s)
-                    : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
+    HIPCHK(v == 4 ? launch_blind_rotate_v4_debug(c->key, B, iters, acc, bara, s)
+                  : launch_blind_rotate_v6_debug(c->key, B, iters, acc, bara, s));
     return TFHE_AMD_OK;
 }
 
@@ -1192,13 +1153,13 @@ extern "C" int tfhe_amd_select_kernel(int br_version) {
 
 extern "C" const char *tfhe_amd_version(void) {
     // one immutable string per (blind-rotation, key-switch) generation pair
-    static char names[10][6][48];
+    static char names[8][6][48];
     static std::once_flag once;
     std::call_once(once, [] {
-        for (int b = 0; b <= 9; b++)
+        for (int b = 0; b <= 7; b++)
             for (int k = 1; k <= 5; k++) {
                 if (b == 0 || b >= 6)
-                    snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v%d ks-v%d", b == 9 ? 9 : 6, k);
+                    snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 fft64 br-v%d ks-v%d", 6, k);
                 else snprintf(names[b][k], sizeof names[b][k], "tfhe_amd gfx950 ntt2x27 br-v%d ks-v%d", b, k);
             }
     });

@@ -16,8 +16,6 @@ struct DeviceKey {
     uint2 *tw4 = nullptr;         // v4 inverse-CT twiddles: uniform [2][16], streams [2][27][64], post-twist [2][16][64]
     double2 *bk_fft = nullptr;    // v6: [kn][4 rows][2 c][8 r][64 L] FFT-domain key / 512 (slot 8 L + r)
     double2 *tw6 = nullptr;       // v6 twiddles: forward [4] + [4][64] x 2, inverse [4][64] x 2, post-twist [8][64]
-    double2 *bk9 = nullptr;       // v9: [kn][2 c][2 h][4 rows][4 t][64 L] FFT-domain key / 512, slot 256 h + 4 L + t
-    double2 *tw9 = nullptr;       // v9 inverse-stage / post-twist lane twiddles [8][64]
     int32_t *ksk = nullptr;       // [kN][kKsT][3][kKsRow]   (digits h = 1..3)
     int32_t *ksk4 = nullptr;      // ks-v4: [126 column blocks][kN][kKsT][3][4]
     int32_t *ksk5 = nullptr;      // ks-v5 (int8 MFMA): [64 N-blocks][kN][64 lanes][16 B] signed key bytes
@@ -29,7 +27,6 @@ struct DeviceKey {
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
 constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64;   // double2 entries (blind_rotate_v6.hip)
-constexpr int kTw9Words = 8 * 64;                                 // double2 entries (blind_rotate_v9.hip)
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -141,17 +138,6 @@ hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, c
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
                                        const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
-                                        const int32_t *bara, hipStream_t s);
-// v9 (4 waves per ciphertext: launches of at most 2 ciphertexts per CU), blind_rotate_v9.hip;
-// guard != null: write the rounding-distance flags as v6
-void build_v9_twiddles(double2 *tw);
-hipError_t launch_bk_fft_to_v9(const double2 *d_bkf, double2 *d_bk9, hipStream_t s);
-hipError_t launch_blind_rotate_v9(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                  int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard = nullptr);
-hipError_t launch_blind_rotate_v9_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
-                                       const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
-                                       const Guard *guard = nullptr);
-hipError_t launch_blind_rotate_v9_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
 // which blind-rotation kernel runs: 0 = default (v6), 1..7 (env TFHE_AMD_BR / tfhe_amd_select_kernel)
 int br_version();

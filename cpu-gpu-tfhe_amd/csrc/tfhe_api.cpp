@@ -576,6 +576,7 @@ struct Coalescer {
     int inside = 0;       // threads inside a Tier-1 gate call on this key
     int in_flight = 0;    // gates taken by running batches
     int running = 0;      // batches running (<= kQueueLanes)
+    int returning = 0;    // callers released by finished batches, expected back with their next gate
     bool collecting = false;   // a leader is waiting for stragglers
     bool lane_busy[kQueueLanes] = {false, false};
     double window_us = -1.0;   // adaptive straggler window (set on first use)
@@ -1030,6 +1031,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     std::unique_lock<std::mutex> lk(q.mu);
     if (q.window_us < 0) q.window_us = coalesce_window_us();
     q.inside += 1;
+    if (q.returning > 0) q.returning -= 1;
     q.pending.push_back(&req);
     q.arrive_cv.notify_all();
     while (!req.done) {
@@ -1043,8 +1045,11 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         q.lane_busy[li] = true;
         q.running += 1;
         q.collecting = true;
-        // stragglers: every thread inside a call and not in a running batch enqueues first
-        auto all_in = [&] { return (int)q.pending.size() >= q.inside - q.in_flight; };
+        // stragglers: every thread inside a call and not in a running batch enqueues first, and so
+        // do the callers the last batch released (an OpenMP team's threads come straight back with
+        // their next gate): without them a team of T threads splits into alternating partial
+        // batches instead of one batch of T
+        auto all_in = [&] { return (int)q.pending.size() >= q.inside - q.in_flight + q.returning; };
         if (!all_in() && q.window_us > 0) {
             const auto t0 = std::chrono::steady_clock::now();
             const bool ok = q.arrive_cv.wait_for(lk, std::chrono::duration<double, std::micro>(q.window_us), all_in);
@@ -1054,6 +1059,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
                 q.window_us = std::min(1000.0, std::max(20.0, 4.0 * q.wait_avg_us + 20.0));
             } else {
                 q.window_us = std::max(20.0, 0.75 * q.window_us);
+                q.returning = 0;   // the released callers did not come back: stop expecting them
             }
         }
         q.collecting = false;
@@ -1077,6 +1083,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         lk.lock();
         for (Tier1Req *x : batch) x->done = true;
         q.in_flight -= (int)batch.size();
+        q.returning += (int)batch.size();   // every caller of the batch (the leader too) leaves and may come back
         q.running -= 1;
         q.lane_busy[li] = false;
         q.batches += 1;

@@ -133,7 +133,7 @@ def select_kernel(generation):
 def available_kernels():
     """The blind-rotation generations this build of the library carries (selection restored)."""
     cur = version().split("br-v")[1].split(" ")[0]
-    out = [v for v in range(1, 10) if lib.tfhe_amd_select_kernel(v) == 0]
+    out = [v for v in range(1, 8) if lib.tfhe_amd_select_kernel(v) == 0]
     lib.tfhe_amd_select_kernel(int(cur) if cur.isdigit() else 0)
     return out
 
