@@ -59,6 +59,19 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
 int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev);
 void tfhe_amd_internal_free(int device, void *dev);
 int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out);
+// Rows of an array of records that each point to their a[500] and hold b (and current_variance):
+// record i is at base + i * stride; its a pointer at a_off, b at b_off, current_variance at v_off
+// (tfhe_api.cpp: LweSample arrays, without the engine knowing the struct)
+struct TfheAmdRows {
+    char *base;
+    size_t stride, a_off, b_off, v_off;
+};
+// a gate batch over such records (tfhe_amd_boots_batch): packed in parallel straight into the pinned
+// staging buffer, pipelined in slices of one round (slice s + 1 packed and copied in while slice s
+// computes, slice s - 1 unpacked meanwhile), current_variance of each result computed on the device
+// from the KSK row variances d_var [1024][8][4] (k_ks_variance) and written with the result
+int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const TfheAmdRows *res,
+                                      const TfheAmdRows *in, int nin, const double *d_var);
 // drops the multi-device context registered for a key (tfhe_gpu_init) when the key is deleted
 void tfhe_amd_internal_forget_multi(const void *bkfft);
 // circuit.cpp: drops every circuit's device state (tables, scratch) held for a context; called by

@@ -13,7 +13,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <memory>
 #include <mutex>
+#include <condition_variable>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -167,6 +170,8 @@ struct TfheAmdContext {
     uint32_t *gstats = nullptr;   // guard counters (engine.h Guard), zeroed at creation
     // pinned host staging for the host API
     int32_t *h_io = nullptr;
+    void *h_u = nullptr;        // pinned readback of extracted samples (Tier-1 variance bookkeeping)
+    size_t h_u_bytes = 0;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -182,6 +187,8 @@ struct TfheAmdContext {
     // sliced host batches (gate_batch_host_sliced): the input copy stream and the events
     hipStream_t copy_in = nullptr;
     hipEvent_t ev_in = nullptr, ev_out[2] = {nullptr, nullptr};
+    double *d_vout = nullptr, *h_vout = nullptr;   // record batches: current_variance per result
+    int vcap = 0;
     std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
     void *mtab = nullptr;       // mixed-gate batches: device row / key-switch tables
     size_t mtab_bytes = 0;
@@ -372,6 +379,9 @@ extern "C" int tfhe_amd_context_destroy(TfheAmdContext *c) {
     for (hipEvent_t e : {c->ev_in, c->ev_out[0], c->ev_out[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->copy_in) (void)hipStreamDestroy(c->copy_in);
+    if (c->h_u) (void)hipHostFree(c->h_u);
+    if (c->h_vout) (void)hipHostFree(c->h_vout);
+    if (c->d_vout) (void)hipFree(c->d_vout);
     free_scratch(c);
     if (c->gstats) (void)hipFree(c->gstats);
     if (!c->shared_key) free_key(c->key);
@@ -773,6 +783,98 @@ int tfhe_amd_internal_l1(TfheAmdContext *c, int op, int B, int iters, const int3
 // Same staging layout as below; slices touch disjoint rows, so a result that aliases an input
 // (the same array) is still read before it is written.
 
+// Host staging copies of the host-pointer paths, split over a few persistent threads: one thread
+// moves ~10 GB/s, so staging a 1 024-gate batch's 4 MB of inputs and 2 MB of results took 0.17 ms
+// of the call's 0.3 ms copy overhead and a 4 096-gate batch's 1 ms (scripts/host_copy_ubench.cpp,
+// profiles/r04b_host_copy_ubench.jsonl: 4 threads 0.05 / 0.19 ms).  Copies below 1 MB in all, and
+// calls that find the pool busy (another context copying), run on the caller's thread.
+// TFHE_AMD_COPY_THREADS sets the pool's helper threads (default 3; 0 = no pool).
+struct CopyJob {
+    void *dst;
+    const void *src;
+    size_t bytes;
+};
+class HostCopyPool {
+public:
+    static HostCopyPool &get() {
+        static HostCopyPool *p = new HostCopyPool();   // never destroyed: helpers idle on their cv at exit
+        return *p;
+    }
+    void copy(const CopyJob *jobs, int n) {
+        size_t total = 0;
+        for (int i = 0; i < n; ++i) total += jobs[i].bytes;
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (helpers_ == 0 || total < (1u << 20) || !busy.owns_lock()) {
+            for (int i = 0; i < n; ++i) memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
+            return;
+        }
+        // one immutable chunk list per job, shared with the helpers that join it (a helper still
+        // finishing an earlier job holds that job's list, never this one's)
+        auto job = std::make_shared<Job>();
+        constexpr size_t kChunk = 256 * 1024;
+        for (int i = 0; i < n; ++i)
+            for (size_t o = 0; o < jobs[i].bytes; o += kChunk)
+                job->chunks.push_back(CopyJob{(char *)jobs[i].dst + o, (const char *)jobs[i].src + o,
+                                              std::min(kChunk, jobs[i].bytes - o)});
+        job->left.store((int)job->chunks.size());
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cur_ = job;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(*job);
+        std::unique_lock<std::mutex> lk(job->mu);
+        job->done.wait(lk, [&] { return job->left.load() == 0; });
+    }
+
+private:
+    struct Job {
+        std::vector<CopyJob> chunks;
+        std::atomic<int> next{0}, left{0};
+        std::mutex mu;
+        std::condition_variable done;
+    };
+    HostCopyPool() {
+        const char *e = getenv("TFHE_AMD_COPY_THREADS");
+        helpers_ = std::max(0, std::min(16, e ? atoi(e) : 3));
+        for (int i = 0; i < helpers_; ++i) std::thread([this] { loop(); }).detach();
+    }
+    static void work(Job &j) {
+        for (;;) {
+            const int i = j.next.fetch_add(1);
+            if (i >= (int)j.chunks.size()) return;
+            memcpy(j.chunks[i].dst, j.chunks[i].src, j.chunks[i].bytes);
+            if (j.left.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> lk(j.mu);
+                j.done.notify_all();
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::shared_ptr<Job> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                job = cur_;
+            }
+            if (job) work(*job);
+        }
+    }
+    int helpers_ = 0;
+    std::mutex run_mu_;                 // one copy job at a time
+    std::mutex mu_;
+    std::condition_variable cv_;
+    uint64_t gen_ = 0;
+    std::shared_ptr<Job> cur_;
+};
+static void host_copy(std::initializer_list<CopyJob> jobs) {
+    HostCopyPool::get().copy(jobs.begin(), (int)jobs.size());
+}
+
 static int host_slice() {   // TFHE_AMD_HOST_SLICE overrides (0: one unsliced batch)
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_HOST_SLICE");
@@ -805,17 +907,20 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
         const int s0 = s * S, n = std::min(S, B - s0);
         const int32_t *ho = h + out0 + R * (size_t)s0;
         HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
-        memcpy(res_a + (size_t)s0 * kn, ho, (size_t)n * kn * 4);
-        memcpy(res_b + s0, ho + (size_t)n * kn, (size_t)n * 4);
+        host_copy({{res_a + (size_t)s0 * kn, ho, (size_t)n * kn * 4}, {res_b + s0, ho + (size_t)n * kn, (size_t)n * 4}});
         return TFHE_AMD_OK;
     };
     for (int s = 0; s < nsl; ++s) {
         const int s0 = s * S, n = std::min(S, B - s0);
         const size_t na = (size_t)n * kn, blk = R * (size_t)nin * s0;
         int32_t *hi = h + blk, *di = d + blk;
-        for (int k = 0; k < nin; ++k) {
-            memcpy(hi + k * na, in_a[k] + (size_t)s0 * kn, na * 4);
-            memcpy(hi + nin * na + (size_t)k * n, in_b[k] + s0, (size_t)n * 4);
+        {
+            std::vector<CopyJob> jobs;
+            for (int k = 0; k < nin; ++k) {
+                jobs.push_back({hi + k * na, in_a[k] + (size_t)s0 * kn, na * 4});
+                jobs.push_back({hi + nin * na + (size_t)k * n, in_b[k] + s0, (size_t)n * 4});
+            }
+            HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
         }
         HIPCHK(hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in));
         HIPCHK(hipEventRecord(c->ev_in, c->copy_in));
@@ -834,6 +939,127 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
         }
     }
     return unstage(nsl - 1);
+}
+
+// Record batches (tfhe_api.cpp tfhe_amd_boots_batch over LweSample arrays).  The records' rows
+// are gathered by the copy pool straight into the pinned staging buffer (no intermediate SoA copy)
+// and the results scattered back the same way; slices of one round are pipelined as in
+// gate_batch_host_sliced (slice s + 1 gathered and copied in on copy_in while slice s computes,
+// slice s - 1 scattered meanwhile).  Each slice's current_variance comes from k_ks_variance on the
+// slice's extracted samples, queued right behind its key switch and copied out with its results.
+static inline int32_t *rec_a(const TfheAmdRows &r, int i) {
+    return *reinterpret_cast<int32_t *const *>(r.base + (size_t)i * r.stride + r.a_off);
+}
+static inline int32_t &rec_b(const TfheAmdRows &r, int i) {
+    return *reinterpret_cast<int32_t *>(r.base + (size_t)i * r.stride + r.b_off);
+}
+static inline double &rec_v(const TfheAmdRows &r, int i) {
+    return *reinterpret_cast<double *>(r.base + (size_t)i * r.stride + r.v_off);
+}
+
+int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const TfheAmdRows *res,
+                                      const TfheAmdRows *in, int nin, const double *d_var) {
+    if (!c || B < 0 || !res || !in || nin < 2 || nin > 3 || !d_var) return TFHE_AMD_E_ARG;
+    if (B == 0) return TFHE_AMD_OK;
+    const bool mux = gate == TFHE_GATE_MUX;
+    if (mux != (nin == 3)) return TFHE_AMD_E_ARG;
+    {
+        int32_t k0, k1, k2;
+        if (!mux && !gate_spec(gate, &k0, &k1, &k2)) return TFHE_AMD_E_ARG;
+    }
+    if (!c->key.has_bk || !c->key.ksk) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
+    TraceScope trace(c);
+    int rc = tfhe_amd_reserve(c, B);
+    if (rc) return rc;
+    if (!c->copy_in) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
+        for (hipEvent_t *e : {&c->ev_in, &c->ev_out[0], &c->ev_out[1]})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    if (B > c->vcap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_vout) (void)hipHostFree(c->h_vout);
+        if (c->d_vout) (void)hipFree(c->d_vout);
+        c->h_vout = nullptr;
+        c->d_vout = nullptr;
+        c->vcap = 0;
+        HIPCHK(hipMalloc(&c->d_vout, sizeof(double) * (size_t)c->cap));
+        HIPCHK(hipHostMalloc(&c->h_vout, sizeof(double) * (size_t)c->cap, hipHostMallocDefault));
+        c->vcap = c->cap;
+    }
+    // staging layout as gate_batch_host_sliced: slice inputs [a_0 | a_1 (| a_2) | b_0 | b_1 (| b_2)]
+    // at word R nin s0, results [res_a | res_b] at 3 R B + R s0
+    constexpr size_t R = kn + 1;
+    int32_t *h = c->h_io, *d = c->io;
+    const size_t out0 = 3 * R * (size_t)B;
+    const int S = host_slice() > 0 ? host_slice() : B;
+    const int nsl = (B + S - 1) / S;
+    const int halves = mux ? 2 : 1;
+    std::vector<CopyJob> jobs;
+    auto scatter = [&](int s) -> int {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        const int32_t *ho = h + out0 + R * (size_t)s0;
+        HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
+        jobs.clear();
+        for (int i = 0; i < n; ++i) jobs.push_back({rec_a(*res, s0 + i), ho + (size_t)i * kn, (size_t)kn * 4});
+        HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+        const int32_t *hb = ho + (size_t)n * kn;
+        for (int i = 0; i < n; ++i) {
+            rec_b(*res, s0 + i) = hb[i];
+            rec_v(*res, s0 + i) = c->h_vout[s0 + i];
+        }
+        return TFHE_AMD_OK;
+    };
+    auto drain = [&] {
+        (void)hipStreamSynchronize(c->copy_in);
+        (void)hipStreamSynchronize(c->stream);
+    };
+    for (int s = 0; s < nsl; ++s) {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        const size_t na = (size_t)n * kn, blk = R * (size_t)nin * s0;
+        int32_t *hi = h + blk, *di = d + blk;
+        jobs.clear();
+        for (int k = 0; k < nin; ++k)
+            for (int i = 0; i < n; ++i) jobs.push_back({hi + k * na + (size_t)i * kn, rec_a(in[k], s0 + i), (size_t)kn * 4});
+        HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+        for (int k = 0; k < nin; ++k)
+            for (int i = 0; i < n; ++i) hi[nin * na + (size_t)k * n + i] = rec_b(in[k], s0 + i);
+        hipError_t e = hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_in, c->copy_in);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+        if (e != hipSuccess) {
+            drain();
+            HIPCHK(e);
+        }
+        const int32_t *da = di, *db = di + nin * na;
+        int32_t *dout = d + out0 + R * (size_t)s0;
+        rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, da, db, da + na, db + n,
+                                     mux ? da + 2 * na : nullptr, mux ? db + 2 * n : nullptr, c->stream);
+        if (rc) {
+            drain();
+            return rc;
+        }
+        e = launch_ks_variance(c->u_a, n, halves, d_var, c->d_vout + s0, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(h + out0 + R * (size_t)s0, dout, R * (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->h_vout + s0, c->d_vout + s0, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_out[s & 1], c->stream);
+        if (e != hipSuccess) {
+            drain();
+            HIPCHK(e);
+        }
+        if (s > 0 && (rc = scatter(s - 1)) != TFHE_AMD_OK) {
+            drain();
+            return rc;
+        }
+    }
+    rc = scatter(nsl - 1);
+    if (rc) drain();
+    return rc;
 }
 
 // host batch: stage inputs into pinned memory, one H2D, the device batch, one D2H (sliced and
@@ -877,9 +1103,13 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     const int nin = mux ? 3 : 2;
     const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
     int32_t *hb = h + nin * A, *db = d + nin * A;
-    for (int k = 0; k < nin; ++k) {
-        memcpy(h + k * A, in_a[k], A * 4);
-        memcpy(hb + (size_t)k * B, in_b[k], (size_t)B * 4);
+    {
+        std::vector<CopyJob> jobs;
+        for (int k = 0; k < nin; ++k) {
+            jobs.push_back({h + k * A, in_a[k], A * 4});
+            jobs.push_back({hb + (size_t)k * B, in_b[k], (size_t)B * 4});
+        }
+        HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
     }
     HIPCHK(hipMemcpyAsync(d, h, (size_t)nin * (A + B) * 4, hipMemcpyHostToDevice, c->stream));
     int32_t *hr = h + 3 * (A + B), *dr = d + 3 * (A + B);
@@ -888,8 +1118,7 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(hr, dr, (A + B) * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    memcpy(res_a, hr, A * 4);
-    memcpy(res_b, hr + A, (size_t)B * 4);
+    host_copy({{res_a, hr, A * 4}, {res_b, hr + A, (size_t)B * 4}});
     return TFHE_AMD_OK;
 }
 
@@ -1039,8 +1268,21 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
     if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap) return TFHE_AMD_E_ARG;
     DeviceScope dev_scope(c->device);
     HIPCHK(dev_scope.rc);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    const size_t bytes = sizeof(int32_t) * (size_t)halves * B * kN;
+    // through the context's pinned readback buffer: a D2H straight into the caller's (pageable,
+    // often freshly allocated) array costs a fixed ~0.3 ms per call, which the Tier-1 queue's
+    // batches paid on their critical path
+    if (bytes > c->h_u_bytes) {
+        if (c->h_u) (void)hipHostFree(c->h_u);
+        c->h_u = nullptr;
+        c->h_u_bytes = 0;
+        HIPCHK(hipHostMalloc(&c->h_u, bytes, hipHostMallocDefault));
+        c->h_u_bytes = bytes;
+    }
+    HIPCHK(hipMemcpyAsync(c->h_u, c->u_a, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(u_a, c->u_a, sizeof(int32_t) * (size_t)halves * B * kN, hipMemcpyDeviceToHost));
+    host_copy({{u_a, c->h_u, bytes}});
     return TFHE_AMD_OK;
 }
 

@@ -582,6 +582,11 @@ struct Coalescer {
     double window_us = -1.0;   // adaptive straggler window (set on first use)
     double wait_avg_us = 0.0;
     long long batches = 0, gates = 0, largest = 0, overlapped = 0;
+    // where a batch's time goes (ms, summed over batches; tfhe_amd_tier1_queue_times):
+    // 0 the leader's straggler wait, 1 packing, 2 the device gate batch (staging, copies, kernels,
+    // synchronize), 3 the key-switch inputs' readback, 4 unpacking, 5 the callers' variance sums
+    double ms[5] = {0, 0, 0, 0, 0};
+    std::atomic<long long> var_ns{0};   // phase 5, added without the queue's lock
 };
 
 struct KeyEntry {
@@ -927,7 +932,16 @@ static int coalesce_window_us() {
 // below takes the single-kind batches).  Inputs are staged before anything is written, so a result
 // may alias any input of its own call; each request gets its key-switch input back, from which its
 // caller sums current_variance as the single-gate path.
-static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
+using Tier1Clock = std::chrono::steady_clock;
+static double ms_since(Tier1Clock::time_point &t) {
+    const Tier1Clock::time_point now = Tier1Clock::now();
+    const double d = std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+    return d;
+}
+
+static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms) {
+    Tier1Clock::time_point t = Tier1Clock::now();
     std::vector<int32_t> buf, u;
     std::vector<int> gates;
     const int total = (int)batch.size();
@@ -947,13 +961,16 @@ static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
             if (q->gate == TFHE_GATE_MUX) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
             rows += q->gate == TFHE_GATE_MUX ? 2 : 1;
         }
+        ms[1] += ms_since(t);
         const int rc = tfhe_amd_gate_batch_mixed_host(l, n, gates.data(), ra, rb, aa, ab, ba, bb, ca, cb);
+        ms[2] += ms_since(t);
         if (rc != TFHE_AMD_OK) {
             for (int i = s0; i < total; ++i) batch[i]->rc = rc;
             return;
         }
         u.resize((size_t)rows * kN);
         check(tfhe_amd_internal_last_extracted(l, rows, 1, u.data()), "variance bookkeeping");
+        ms[3] += ms_since(t);
         for (int i = 0, r = 0; i < n; ++i) {   // rows in request order: a MUX has two (u1 + u2)
             Tier1Req *q = batch[s0 + i];
             memcpy(q->r->a, ra + (size_t)i * kn, kn * 4);
@@ -967,15 +984,17 @@ static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
                 r += 1;
             }
         }
+        ms[4] += ms_since(t);
     }
 }
 
-static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch) {
+static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms) {
     for (const Tier1Req *q : batch)
         if (q->gate != batch[0]->gate) {
-            run_tier1_mixed(l, batch);
+            run_tier1_mixed(l, batch, ms);
             return;
         }
+    Tier1Clock::time_point t = Tier1Clock::now();
     // one gate kind: host gate batches of one unsliced round each, so that each round's
     // key-switch inputs are still in the lane's scratch for the variance bookkeeping
     std::vector<int32_t> buf, u;
@@ -991,17 +1010,20 @@ static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
         memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
         if (mux) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
     }
+    ms[1] += ms_since(t);
     const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
     for (int s0 = 0; s0 < n; s0 += round) {
         const int m = std::min(round, n - s0);
         const size_t o = (size_t)s0 * kn;
         const int rc = tfhe_amd_gate_batch_host(l, gate, m, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
                                                 mux ? ca + o : nullptr, mux ? cb + s0 : nullptr);
+        ms[2] += ms_since(t);
         if (rc != TFHE_AMD_OK) {
             for (int i = s0; i < n; ++i) batch[i]->rc = rc;
             return;
         }
         ks_input_of_last(l, m, mux ? 2 : 1, u);
+        ms[3] += ms_since(t);
         for (int i = 0; i < m; ++i) {
             Tier1Req *q = batch[s0 + i];
             memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
@@ -1010,6 +1032,7 @@ static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
             // queue's critical path): 8 192 table reads per gate
             q->u.assign(u.begin() + (size_t)i * kN, u.begin() + (size_t)(i + 1) * kN);
         }
+        ms[4] += ms_since(t);
     }
 }
 
@@ -1050,6 +1073,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         // their next gate): without them a team of T threads splits into alternating partial
         // batches instead of one batch of T
         auto all_in = [&] { return (int)q.pending.size() >= q.inside - q.in_flight + q.returning; };
+        double bms[5] = {0, 0, 0, 0, 0};
         if (!all_in() && q.window_us > 0) {
             const auto t0 = std::chrono::steady_clock::now();
             const bool ok = q.arrive_cv.wait_for(lk, std::chrono::duration<double, std::micro>(q.window_us), all_in);
@@ -1061,6 +1085,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
                 q.window_us = std::max(20.0, 0.75 * q.window_us);
                 q.returning = 0;   // the released callers did not come back: stop expecting them
             }
+            bms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         }
         q.collecting = false;
         std::vector<Tier1Req *> batch;
@@ -1079,8 +1104,9 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
             l = e->qlane[li];
         }
         if (!l) die_dramatically("tfhe_amd: cannot create the Tier-1 queue's GPU lane");
-        if (!batch.empty()) run_tier1_batch(l, batch);
+        if (!batch.empty()) run_tier1_batch(l, batch, bms);
         lk.lock();
+        for (int k = 0; k < 5; ++k) q.ms[k] += bms[k];
         for (Tier1Req *x : batch) x->done = true;
         q.in_flight -= (int)batch.size();
         q.returning += (int)batch.size();   // every caller of the batch (the leader too) leaves and may come back
@@ -1096,7 +1122,9 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     q.arrive_cv.notify_all();   // a leader may be waiting for this thread
     lk.unlock();
     check(req.rc, "gate");
+    const Tier1Clock::time_point tv = Tier1Clock::now();
     r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
+    q.var_ns += (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Tier1Clock::now() - tv).count();
 }
 
 // Builds the key's Tier-1 device context (key upload + conversion, HIP initialisation, the
@@ -1128,6 +1156,28 @@ EXPORT int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk
     if (batches) *batches = b;
     if (gates) *gates = g;
     if (largest) *largest = m;
+    return TFHE_AMD_OK;
+}
+
+EXPORT int tfhe_amd_tier1_queue_times(const TFheGateBootstrappingCloudKeySet *bk, double *ms, int reset) {
+    if (!bk || !bk->bkFFT) return TFHE_AMD_E_ARG;
+    std::shared_ptr<KeyEntry> e;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find(bk->bkFFT);
+        if (it != g_reg.end()) e = it->second;
+    }
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    if (e) {
+        std::lock_guard<std::mutex> lk(e->q.mu);
+        for (int k = 0; k < 5; ++k) {
+            m[k] = e->q.ms[k];
+            if (reset) e->q.ms[k] = 0;
+        }
+        m[5] = 1e-6 * (double)(reset ? e->q.var_ns.exchange(0) : e->q.var_ns.load());
+    }
+    if (ms)
+        for (int k = 0; k < 6; ++k) ms[k] = m[k];
     return TFHE_AMD_OK;
 }
 
@@ -1173,63 +1223,43 @@ int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, in
     return tfhe_amd_gate_batch_host(l, gate, B, res_a, res_b, a_a, a_b, b_a, b_b, c_a, c_b);
 }
 
-// batched convenience over LweSample arrays (SoA staging on the host)
+// batched convenience over LweSample arrays: the engine gathers the records' rows straight into
+// its pinned staging buffer and scatters the results back, pipelined in slices of one round, with
+// current_variance computed on the device (tfhe_amd_internal_gate_batch_rows).  result may be the
+// same array as an input.
+static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
+    // the KSK row variances on the device, once per key: each slice's current_variance is summed by
+    // k_ks_variance (the reference's order of double adds) instead of on the host from the slice's
+    // 4 KB-per-gate key-switch inputs (B = 1024: ~16 ms of host work and a 4 MB copy)
+    std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->d_var) {
+        const LweKeySwitchKey *ks = bk->bkFFT->ks;
+        std::vector<double> var((size_t)kN * kKsT * kKsBase);
+        for (int i = 0; i < kN; ++i)
+            for (int j = 0; j < kKsT; ++j)
+                for (int h = 0; h < kKsBase; ++h)
+                    var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
+        void *dv = nullptr;
+        if (tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv)) return nullptr;
+        e->d_var = (double *)dv;
+    }
+    return e->d_var;
+}
+
 EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
                                 const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk) {
     if (!bk || !bk->bkFFT || B < 0 || !result || !a || !b) return TFHE_AMD_E_ARG;
     if (B == 0) return TFHE_AMD_OK;
     if (gate == TFHE_GATE_MUX && !c) return TFHE_AMD_E_ARG;
+    if (gate != TFHE_GATE_MUX) c = nullptr;
     TfheAmdContext *l = lane_for(bk->bkFFT, nullptr);
-    const size_t A = (size_t)B * kn;
-    std::vector<int32_t> buf(4 * A + 4 * (size_t)B);
-    int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
-    int32_t *ab = ra + A, *bb = ab + B, *cb = bb + B, *rb = cb + B;
-    for (int i = 0; i < B; i++) {
-        memcpy(aa + (size_t)i * kn, a[i].a, kn * 4); ab[i] = a[i].b;
-        memcpy(ba + (size_t)i * kn, b[i].a, kn * 4); bb[i] = b[i].b;
-        if (c) { memcpy(ca + (size_t)i * kn, c[i].a, kn * 4); cb[i] = c[i].b; }
-    }
-    // in rounds the host path runs unsliced (at most 1024, or TFHE_AMD_HOST_SLICE if smaller), so
-    // that each round's key-switch inputs are all still in the lane's scratch for the variance
-    // bookkeeping
-    const int halves = gate == TFHE_GATE_MUX ? 2 : 1;
-    const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
-    // the KSK row variances on the device, once per key: each round's current_variance is then
-    // summed by k_ks_variance (the reference's order of double adds) instead of on the host from
-    // the round's 4 KB-per-gate key-switch inputs (B = 1024: ~16 ms of host work and a 4 MB copy)
-    double *d_var = nullptr;
-    {
-        std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
-        std::lock_guard<std::mutex> lk(e->mu);
-        if (!e->d_var) {
-            const LweKeySwitchKey *ks = bk->bkFFT->ks;
-            std::vector<double> var((size_t)kN * kKsT * kKsBase);
-            for (int i = 0; i < kN; ++i)
-                for (int j = 0; j < kKsT; ++j)
-                    for (int h = 0; h < kKsBase; ++h)
-                        var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
-            void *dv = nullptr;
-            const int rc = tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv);
-            if (rc) return rc;
-            e->d_var = (double *)dv;
-        }
-        d_var = e->d_var;
-    }
-    std::vector<double> v;
-    for (int s0 = 0; s0 < B; s0 += round) {
-        const int n = B - s0 < round ? B - s0 : round;
-        const size_t o = (size_t)s0 * kn;
-        int rc = tfhe_amd_gate_batch_host(l, gate, n, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
-                                          c ? ca + o : nullptr, c ? cb + s0 : nullptr);
-        if (rc) return rc;
-        v.resize(n);
-        rc = tfhe_amd_internal_ks_variance(l, n, halves, d_var, v.data());
-        if (rc) return rc;
-        for (int i = 0; i < n; i++) result[s0 + i].current_variance = v[i];
-    }
-    for (int i = 0; i < B; i++) {
-        memcpy(result[i].a, ra + (size_t)i * kn, kn * 4);
-        result[i].b = rb[i];
-    }
-    return TFHE_AMD_OK;
+    const double *d_var = ks_variance_table(bk);
+    if (!d_var) return TFHE_AMD_E_HIP;
+    auto rows = [](const LweSample *x) {
+        return TfheAmdRows{reinterpret_cast<char *>(const_cast<LweSample *>(x)), sizeof(LweSample),
+                           offsetof(LweSample, a), offsetof(LweSample, b), offsetof(LweSample, current_variance)};
+    };
+    const TfheAmdRows res = rows(result), in[3] = {rows(a), rows(b), c ? rows(c) : rows(a)};
+    return tfhe_amd_internal_gate_batch_rows(l, gate, B, &res, in, c ? 3 : 2, d_var);
 }

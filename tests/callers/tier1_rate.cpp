@@ -70,6 +70,7 @@ int main(int argc, char **argv) {
         for (int t = 0; t < T; t++) bootsNAND(&out[t], &a[t], &b[t], bk);
         for (int i = 0; i < n; i++) lweCopy(&out[i], &a[i], lp);
         tfhe_amd_tier1_queue_stats(bk, nullptr, nullptr, nullptr, 1);
+        tfhe_amd_tier1_queue_times(bk, nullptr, 1);
         t0 = omp_get_wtime();
 #pragma omp parallel for num_threads(T) schedule(static)
         for (int i = 0; i < n; i++) {
@@ -79,14 +80,19 @@ int main(int argc, char **argv) {
         const double dt = omp_get_wtime() - t0;
         long long nb = 0, ng = 0, big = 0;
         tfhe_amd_tier1_queue_stats(bk, &nb, &ng, &big, 1);
+        double qms[6];
+        tfhe_amd_tier1_queue_times(bk, qms, 1);
         int bad = 0;
         for (int i = 0; i < n; i++) bad += !same(&out[i], &seq[i], dim);
         mismatches += bad;
-        char line[256];
+        char line[512];
+        const double pb = nb ? 1.0 / nb : 0.0;   // per batch
         snprintf(line, sizeof line,
                  "%s{\"threads\": %d, \"gates\": %d, \"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, "
-                 "\"batches\": %lld, \"mean_batch\": %.2f, \"largest_batch\": %lld}",
-                 runs.empty() ? "" : ", ", T, n, dt, n / dt, bad, nb, nb ? (double)ng / nb : 0.0, big);
+                 "\"batches\": %lld, \"mean_batch\": %.2f, \"largest_batch\": %lld, \"ms_per_batch\": {\"wait\": %.3f, "
+                 "\"pack\": %.3f, \"device\": %.3f, \"readback\": %.3f, \"unpack\": %.3f, \"variance_per_caller\": %.4f}}",
+                 runs.empty() ? "" : ", ", T, n, dt, n / dt, bad, nb, nb ? (double)ng / nb : 0.0, big, qms[0] * pb,
+                 qms[1] * pb, qms[2] * pb, qms[3] * pb, qms[4] * pb, ng ? qms[5] / ng : 0.0);
         runs += line;
     }
     // mixed kinds: gate i is kind i mod 11 (the 10 binary gates and MUX), as threads of a real

@@ -272,6 +272,42 @@ int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const do
     }
     return TFHE_AMD_OK;
 }
+// record batches (tfhe_amd_boots_batch): gather, the stand-in batch, variance, scatter, in slices
+int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const TfheAmdRows *res,
+                                      const TfheAmdRows *in, int nin, const double *d_var) {
+    if (!c || B < 0 || !res || !in || nin < 2 || nin > 3 || !d_var) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    auto ra_of = [](const TfheAmdRows &r, int i) {
+        return *reinterpret_cast<int32_t *const *>(r.base + (size_t)i * r.stride + r.a_off);
+    };
+    auto rb_of = [](const TfheAmdRows &r, int i) -> int32_t & {
+        return *reinterpret_cast<int32_t *>(r.base + (size_t)i * r.stride + r.b_off);
+    };
+    const int S = 1024, halves = gate == TFHE_GATE_MUX ? 2 : 1;
+    for (int s0 = 0; s0 < B; s0 += S) {
+        const int n = std::min(S, B - s0);
+        std::vector<int32_t> ia((size_t)3 * n * kn), ib((size_t)3 * n), oa((size_t)n * kn), ob(n);
+        for (int k = 0; k < nin; ++k)
+            for (int i = 0; i < n; ++i) {
+                memcpy(&ia[((size_t)k * n + i) * kn], ra_of(in[k], s0 + i), kn * 4);
+                ib[(size_t)k * n + i] = rb_of(in[k], s0 + i);
+            }
+        const size_t na = (size_t)n * kn;
+        int rc = rows_batch(c, n, nullptr, gate, oa.data(), ob.data(), ia.data(), ib.data(), ia.data() + na,
+                            ib.data() + n, nin > 2 ? ia.data() + 2 * na : nullptr, nin > 2 ? ib.data() + 2 * n : nullptr);
+        if (rc) return rc;
+        std::vector<double> v(n);
+        rc = tfhe_amd_internal_ks_variance(c, n, halves, d_var, v.data());
+        if (rc) return rc;
+        for (int i = 0; i < n; ++i) {
+            char *rec = res->base + (size_t)(s0 + i) * res->stride;
+            memcpy(*reinterpret_cast<int32_t **>(rec + res->a_off), &oa[(size_t)i * kn], kn * 4);
+            *reinterpret_cast<int32_t *>(rec + res->b_off) = ob[i];
+            *reinterpret_cast<double *>(rec + res->v_off) = v[i];
+        }
+    }
+    return TFHE_AMD_OK;
+}
 
 // ---- circuits: the engine wrapper + stand-in launches (rows -> u, key switch -> wires, linear)
 int tfhe_amd_circuit_run_dev_impl(uint64_t ctx_uid, const DeviceKey &key, int device, hipStream_t s,

@@ -163,6 +163,51 @@ static void test_tier1(const TFheGateBootstrappingParameterSet *params, const TF
     }
 }
 
+// ---- LweSample-array batches (tfhe_amd_boots_batch) from several threads, each on its own arrays
+// (one in place: result = input a; one of two slices), against the single-gate calls one by one
+static void test_boots_batch(const TFheGateBootstrappingParameterSet *params, const TFheGateBootstrappingCloudKeySet *bk,
+                             int threads) {
+    const int sizes[] = {1, 7, 64, 1100};
+    std::vector<LweSample *> a(threads), b(threads), c(threads), r(threads), ref(threads);
+    std::vector<int> n(threads), g(threads);
+    for (int t = 0; t < threads; ++t) {
+        n[t] = sizes[t % 4];
+        g[t] = kGates[t % 10];
+        a[t] = new_gate_bootstrapping_ciphertext_array(n[t], params);
+        b[t] = new_gate_bootstrapping_ciphertext_array(n[t], params);
+        c[t] = new_gate_bootstrapping_ciphertext_array(n[t], params);
+        r[t] = new_gate_bootstrapping_ciphertext_array(n[t], params);
+        ref[t] = new_gate_bootstrapping_ciphertext_array(n[t], params);
+        for (int i = 0; i < n[t]; ++i) {
+            fill(&a[t][i], 7000 + 3 * i + t);
+            fill(&b[t][i], 9000 + 5 * i + t);
+            fill(&c[t][i], 11000 + 7 * i + t);
+            gate_call(g[t], &ref[t][i], &a[t][i], &b[t][i], &c[t][i], bk);
+        }
+    }
+    std::vector<std::thread> th;
+    std::vector<int> rcs(threads, 0);
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            LweSample *out = t % 3 == 0 ? a[t] : r[t];   // in place on every third thread
+            rcs[t] = tfhe_amd_boots_batch(g[t], out, a[t], b[t], c[t], n[t], bk);
+        });
+    for (auto &x : th) x.join();
+    int bad = 0, badv = 0;
+    for (int t = 0; t < threads; ++t) {
+        CHECK(rcs[t] == TFHE_AMD_OK, "boots_batch: thread %d rc %d", t, rcs[t]);
+        const LweSample *out = t % 3 == 0 ? a[t] : r[t];
+        for (int i = 0; i < n[t]; ++i) {
+            bad += !same(snap(&out[i]), snap(&ref[t][i]));
+            badv += out[i].current_variance != ref[t][i].current_variance;
+        }
+    }
+    CHECK(bad == 0 && badv == 0, "boots_batch: %d results and %d variances differ from single gates", bad, badv);
+    printf("boots_batch: %d threads (sizes 1-1100, in place on every third), equal to single gates\n", threads);
+    for (int t = 0; t < threads; ++t)
+        for (LweSample *x : {a[t], b[t], c[t], r[t], ref[t]}) delete_gate_bootstrapping_ciphertext_array(n[t], x);
+}
+
 // ---- Tier-2 multi-device registry: tfhe_gpu_boots_batch on a key while tfhe_gpu_init
 // re-registers it, and other keys are imported, registered, used and deleted
 static void soa(int B, int seed, std::vector<int32_t> &a, std::vector<int32_t> &b) {
@@ -286,6 +331,7 @@ int main(int argc, char **argv) {
     export_tfheGateBootstrappingCloudKeySet_toStream(out, bk);
     const std::string cloud_bytes = out.str();
     test_tier1(params, bk, threads, steps);
+    test_boots_batch(params, bk, 8);
     test_multi(bk, cloud_bytes, 8);
     test_circuits(bk, 8);
     delete_gate_bootstrapping_secret_keyset(key);
