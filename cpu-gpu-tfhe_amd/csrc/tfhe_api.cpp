@@ -544,14 +544,24 @@ EXPORT int bootsSymDecrypt(const LweSample *sample, const TFheGateBootstrappingS
 static std::atomic<int> g_default_device{0};
 
 // One pending single-gate call of the coalescing queue (below).
+// Its caller sleeps on the request's own condition variable, so that a finished batch wakes only
+// its own callers (and a freed lane one new leader) instead of every thread inside a call.
 struct Tier1Req {
     int gate;
     LweSample *r;
     const LweSample *a, *b, *c;
-    bool taken = false;   // in a running batch
-    bool done = false;
+    bool taken = false;   // in a running batch (queue lock)
     int rc = TFHE_AMD_OK;
     std::vector<int32_t> u;   // its key-switch input: the caller derives current_variance from it
+    std::mutex m;             // wake-up of the caller: done (its batch finished) or a call to lead
+    std::condition_variable cv;
+    bool signaled = false, done = false;
+    void wake(bool finished) {   // the request may be gone once m is released with done set
+        std::lock_guard<std::mutex> lk(m);
+        done = done || finished;
+        signaled = true;
+        cv.notify_one();
+    }
 };
 
 // Coalescing queue of the Tier-1 gates of one key ("per-thread streams or a
@@ -564,14 +574,17 @@ struct Tier1Req {
 // that lane — one gate kind as a gate batch, several kinds as one mixed launch per 512 gates.
 // Two lanes (own stream + scratch each) alternate, so batch k + 1 is staged and launched while
 // batch k is still on the GPU or being unstaged: the queue no longer serialises a whole batch's
-// host work with the next one.  A lone thread is its own leader at once (B = 1 latency).
+// host work with the next one.  A lone thread is its own leader at once (B = 1 latency).  Callers
+// sleep on their own request: a finished batch's leader does its callers' bookkeeping and wakes
+// exactly them, and a freed lane wakes the oldest pending caller to lead (no wake-up of every
+// thread in the call per batch, which serialised 64 threads on the queue lock).
 // The window adapts to the callers: it starts at TFHE_AMD_TIER1_WINDOW_US (default 200 us),
 // follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
 // shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [20, 1000] us.
 constexpr int kQueueLanes = 2;
 struct Coalescer {
     std::mutex mu;
-    std::condition_variable done_cv, arrive_cv;
+    std::condition_variable arrive_cv;   // a collecting leader waits here for stragglers
     std::vector<Tier1Req *> pending;
     int inside = 0;       // threads inside a Tier-1 gate call on this key
     int in_flight = 0;    // gates taken by running batches
@@ -1050,18 +1063,35 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     }
     std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
     Coalescer &q = e->q;
-    Tier1Req req{gate, r, a, b, c};
+    Tier1Req req;
+    req.gate = gate;
+    req.r = r;
+    req.a = a;
+    req.b = b;
+    req.c = c;
     std::unique_lock<std::mutex> lk(q.mu);
     if (q.window_us < 0) q.window_us = coalesce_window_us();
     q.inside += 1;
     if (q.returning > 0) q.returning -= 1;
     q.pending.push_back(&req);
-    q.arrive_cv.notify_all();
-    while (!req.done) {
-        if (req.taken || q.collecting || q.running >= kQueueLanes || q.pending.empty()) {
-            q.done_cv.wait(lk);
-            continue;
+    q.arrive_cv.notify_all();   // a collecting leader may be waiting for this thread
+    // a free lane and no leader collecting: the oldest pending request's thread is asked to lead
+    auto appoint = [&] {
+        if (!q.collecting && q.running < kQueueLanes && !q.pending.empty() && q.pending.front() != &req)
+            q.pending.front()->wake(false);
+    };
+    for (;;) {
+        if (!req.taken && !q.collecting && q.running < kQueueLanes) break;   // lead the next batch
+        lk.unlock();
+        {
+            std::unique_lock<std::mutex> rl(req.m);
+            req.cv.wait(rl, [&] { return req.signaled; });
+            req.signaled = false;
+            if (req.done) break;
         }
+        lk.lock();
+    }
+    if (!req.done) {
         // this thread leads the next batch, on a free lane
         int li = 0;
         while (q.lane_busy[li]) ++li;
@@ -1093,7 +1123,6 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         for (Tier1Req *x : batch) x->taken = true;
         q.in_flight += (int)batch.size();
         if (q.running > 1) q.overlapped += 1;
-        q.done_cv.notify_all();   // another waiting thread may lead the next batch on the other lane
         lk.unlock();
         // the queue's own lanes (stream + scratch), not the leader thread's: a thread that only
         // ever enqueues needs no lane, and leaders change from batch to batch
@@ -1104,23 +1133,25 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
             l = e->qlane[li];
         }
         if (!l) die_dramatically("tfhe_amd: cannot create the Tier-1 queue's GPU lane");
-        if (!batch.empty()) run_tier1_batch(l, batch, bms);
+        run_tier1_batch(l, batch, bms);
         lk.lock();
         for (int k = 0; k < 5; ++k) q.ms[k] += bms[k];
-        for (Tier1Req *x : batch) x->done = true;
-        q.in_flight -= (int)batch.size();
-        q.returning += (int)batch.size();   // every caller of the batch (the leader too) leaves and may come back
+        const int n = (int)batch.size();
+        q.in_flight -= n;
+        q.inside -= n;       // every caller of the batch (the leader too) leaves now ...
+        q.returning += n;    // ... and may come back with its next gate
         q.running -= 1;
         q.lane_busy[li] = false;
         q.batches += 1;
-        q.gates += (long long)batch.size();
-        q.largest = std::max(q.largest, (long long)batch.size());
-        q.done_cv.notify_all();
+        q.gates += n;
+        q.largest = std::max(q.largest, (long long)n);
         q.arrive_cv.notify_all();   // a collecting leader's expected count changed
+        appoint();                  // this lane is free again
+        lk.unlock();
+        for (Tier1Req *x : batch)
+            if (x != &req) x->wake(true);   // x may return (and its request vanish) from here on
     }
-    q.inside -= 1;
-    q.arrive_cv.notify_all();   // a leader may be waiting for this thread
-    lk.unlock();
+    // (otherwise: done by another thread's batch, whose leader did this call's bookkeeping)
     check(req.rc, "gate");
     const Tier1Clock::time_point tv = Tier1Clock::now();
     r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());

@@ -142,8 +142,8 @@ def test_tier1_current_variance_as_reference(keyset, okey, rng):
 @pytest.mark.gpu
 def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
     """tfhe_amd_boots_batch over LweSample arrays (SURVEY.md §8(b)'s LweSample convenience overload):
-    1 100 NAND gates (two rounds: 1 024 + 76) and 33 MUX gates give the Torus32 words of the device
-    batch path, and current_variance — summed on the device by k_ks_variance in the reference's order
+    1 100 NAND gates (two pipelined slices: 1 024 + 76) and 33 MUX gates give the Torus32 words of the
+    device batch path, also in place (result = the first input array), and current_variance — summed on the device by k_ks_variance in the reference's order
     of double adds — equals, bit for bit, the Tier-1 gates' (summed on the host) on sampled rows."""
     import ctypes
     import time
@@ -180,22 +180,32 @@ def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
         for (p, s), (a, b) in zip(arrs[:nin], host):
             fill(s, a, b)
         res_p, res = arrs[nin]
-        t0 = time.perf_counter()
-        rc = lib.tfhe_amd_boots_batch(T.GATES[gate], P(res_p), P(arrs[0][0]), P(arrs[1][0]),
-                                      P(arrs[2][0]) if nin == 3 else None, B, P(cloud))
-        dt = time.perf_counter() - t0
-        assert rc == 0
+        dts = []
+        for _ in range(3):   # the first call also sizes the context's staging and variance buffers
+            t0 = time.perf_counter()
+            rc = lib.tfhe_amd_boots_batch(T.GATES[gate], P(res_p), P(arrs[0][0]), P(arrs[1][0]),
+                                          P(arrs[2][0]) if nin == 3 else None, B, P(cloud))
+            dts.append(time.perf_counter() - t0)
+            assert rc == 0
         got_a = np.array([np.ctypeslib.as_array(res[k].a, (500,)) for k in range(B)])
         got_b = np.array([res[k].b for k in range(B)], dtype=np.int32)
         want = ctx.gate_host(gate, *[v for hb in host for v in hb])
         assert np.array_equal(got_a, want[0]) and np.array_equal(got_b, want[1]), gate
-        print(f"tfhe_amd_boots_batch {gate} B={B}: {dt * 1e3:.1f} ms")
+        print(f"tfhe_amd_boots_batch {gate} B={B}: {min(dts[1:]) * 1e3:.2f} ms warm ({dts[0] * 1e3:.1f} ms first)")
         one = arrays(1, 1)[0]
         for k in np.unique(np.concatenate([[0, B - 1, min(1023, B - 1), min(1024, B - 1)],
                                            rng.choice(B, 12, replace=False)])):
             ins = [P(ctypes.addressof(arrs[j][1][k])) for j in range(nin)]
             (lib.bootsMUX if gate == "MUX" else lib.bootsNAND)(P(one[0]), *ins, P(cloud))
             assert one[1][0].current_variance == res[k].current_variance > 0, (gate, k)
+        # in place: the result array is the first input array (slices of 1 024 + 76 alias row by row)
+        rc = lib.tfhe_amd_boots_batch(T.GATES[gate], P(arrs[0][0]), P(arrs[0][0]), P(arrs[1][0]),
+                                      P(arrs[2][0]) if nin == 3 else None, B, P(cloud))
+        assert rc == 0
+        got_a = np.array([np.ctypeslib.as_array(arrs[0][1][k].a, (500,)) for k in range(B)])
+        got_b = np.array([arrs[0][1][k].b for k in range(B)], dtype=np.int32)
+        assert np.array_equal(got_a, want[0]) and np.array_equal(got_b, want[1]), (gate, "in place")
+        assert all(arrs[0][1][k].current_variance == res[k].current_variance for k in range(B))
         for p, _ in arrs + [one]:
             lib.delete_gate_bootstrapping_ciphertext_array(B if p != one[0] else 1, P(p))
 
