@@ -611,15 +611,32 @@ __global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ 
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= B) return;
     const int32_t *u = u_a + (size_t)g * kN;
-    const int32_t *u2 = halves == 2 ? u_a + ((size_t)B + g) * kN : nullptr;
+    const int32_t *u2 = halves == 2 ? u_a + ((size_t)B + g) * kN : u;
     double v = 0.0;
-    for (int i = 0; i < kN; ++i) {
-        const uint32_t aibar = (uint32_t)u[i] + (u2 ? (uint32_t)u2[i] : 0u) + kKsPrecOffset;
+    // 4 coefficients = 32 table reads in flight per round (a one-thread-per-sample sum is a chain
+    // of dependent adds; its loads must not be): a zero digit reads entry 0 of its row and adds
+    // +0.0, which leaves v (>= +0) unchanged, exactly as skipping it
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < kN; i0 += U) {
+        uint32_t ab[U];
 #pragma unroll
-        for (int j = 0; j < kKsT; ++j) {
-            const uint32_t aij = (aibar >> (32 - (j + 1) * kKsBasebit)) & (uint32_t)(kKsBase - 1);
-            if (aij) v = __dadd_rn(v, var[(i * kKsT + j) * kKsBase + aij]);
-        }
+        for (int k = 0; k < U; ++k)
+            ab[k] = (uint32_t)u[i0 + k] + (halves == 2 ? (uint32_t)u2[i0 + k] : 0u) + kKsPrecOffset;
+        double t[U][kKsT];
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+#pragma unroll
+            for (int j = 0; j < kKsT; ++j) {
+                const uint32_t aij = (ab[k] >> (32 - (j + 1) * kKsBasebit)) & (uint32_t)(kKsBase - 1);
+                t[k][j] = var[((i0 + k) * kKsT + j) * kKsBase + aij];
+            }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+#pragma unroll
+            for (int j = 0; j < kKsT; ++j) {
+                const uint32_t aij = (ab[k] >> (32 - (j + 1) * kKsBasebit)) & (uint32_t)(kKsBase - 1);
+                v = __dadd_rn(v, aij ? t[k][j] : 0.0);
+            }
     }
     out[g] = v;
 }

@@ -551,6 +551,7 @@ struct Tier1Req {
     LweSample *r;
     const LweSample *a, *b, *c;
     bool taken = false;   // in a running batch (queue lock)
+    bool var_done = false;   // its batch wrote r->current_variance (device-side sum)
     int rc = TFHE_AMD_OK;
     std::vector<int32_t> u;   // its key-switch input: the caller derives current_variance from it
     std::mutex m;             // wake-up of the caller: done (its batch finished) or a call to lead
@@ -940,6 +941,26 @@ static int coalesce_window_us() {
     return v;
 }
 
+static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
+    // the KSK row variances on the device, once per key: each slice's current_variance is summed by
+    // k_ks_variance (the reference's order of double adds) instead of on the host from the slice's
+    // 4 KB-per-gate key-switch inputs (B = 1024: ~16 ms of host work and a 4 MB copy)
+    std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->d_var) {
+        const LweKeySwitchKey *ks = bk->bkFFT->ks;
+        std::vector<double> var((size_t)kN * kKsT * kKsBase);
+        for (int i = 0; i < kN; ++i)
+            for (int j = 0; j < kKsT; ++j)
+                for (int h = 0; h < kKsBase; ++h)
+                    var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
+        void *dv = nullptr;
+        if (tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv)) return nullptr;
+        e->d_var = (double *)dv;
+    }
+    return e->d_var;
+}
+
 // A batch of queued gates holding more than one gate kind runs as ONE mixed launch per 512 gates
 // (tfhe_amd_gate_batch_mixed_host: one blind rotation + one key switch for all kinds; run_tier1_batch
 // below takes the single-kind batches).  Inputs are staged before anything is written, so a result
@@ -1001,52 +1022,48 @@ static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
     }
 }
 
-static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms) {
+// One gate kind: the engine's record path (tfhe_amd_internal_gate_batch_rows) gathers each request's
+// input rows straight into the lane's pinned staging, scatters the results straight into the callers'
+// result samples and sums current_variance on the device, so the batch has no intermediate SoA copies,
+// no readback of the key-switch inputs and no per-caller variance sums.
+static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms,
+                            const double *d_var) {
     for (const Tier1Req *q : batch)
         if (q->gate != batch[0]->gate) {
             run_tier1_mixed(l, batch, ms);
             return;
         }
     Tier1Clock::time_point t = Tier1Clock::now();
-    // one gate kind: host gate batches of one unsliced round each, so that each round's
-    // key-switch inputs are still in the lane's scratch for the variance bookkeeping
-    std::vector<int32_t> buf, u;
     const int gate = batch[0]->gate, n = (int)batch.size();
     const bool mux = gate == TFHE_GATE_MUX;
-    const size_t A = (size_t)n * kn;
-    buf.resize(4 * A + 4 * (size_t)n);
-    int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
-    int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
+    // shallow copies of the samples: the a pointers and b values (taken before anything is written,
+    // so a result may alias an input of its own call)
+    std::vector<LweSample> rec((size_t)4 * n);
+    LweSample *ra = rec.data(), *rb = ra + n, *rc3 = rb + n, *rr = rc3 + n;
     for (int i = 0; i < n; ++i) {
         const Tier1Req *q = batch[i];
-        memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
-        memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
-        if (mux) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
+        ra[i].a = q->a->a; ra[i].b = q->a->b;
+        rb[i].a = q->b->a; rb[i].b = q->b->b;
+        if (mux) { rc3[i].a = q->c->a; rc3[i].b = q->c->b; }
+        rr[i].a = q->r->a;
     }
+    auto rows = [](LweSample *x) {
+        return TfheAmdRows{reinterpret_cast<char *>(x), sizeof(LweSample), offsetof(LweSample, a),
+                           offsetof(LweSample, b), offsetof(LweSample, current_variance)};
+    };
+    const TfheAmdRows res = rows(rr), in[3] = {rows(ra), rows(rb), rows(rc3)};
     ms[1] += ms_since(t);
-    const int round = std::min(1024, tfhe_amd_internal_unsliced_max());
-    for (int s0 = 0; s0 < n; s0 += round) {
-        const int m = std::min(round, n - s0);
-        const size_t o = (size_t)s0 * kn;
-        const int rc = tfhe_amd_gate_batch_host(l, gate, m, ra + o, rb + s0, aa + o, ab + s0, ba + o, bb + s0,
-                                                mux ? ca + o : nullptr, mux ? cb + s0 : nullptr);
-        ms[2] += ms_since(t);
-        if (rc != TFHE_AMD_OK) {
-            for (int i = s0; i < n; ++i) batch[i]->rc = rc;
-            return;
-        }
-        ks_input_of_last(l, m, mux ? 2 : 1, u);
-        ms[3] += ms_since(t);
-        for (int i = 0; i < m; ++i) {
-            Tier1Req *q = batch[s0 + i];
-            memcpy(q->r->a, ra + o + (size_t)i * kn, kn * 4);
-            q->r->b = rb[s0 + i];
-            // current_variance is summed by each caller after the batch (in parallel, off the
-            // queue's critical path): 8 192 table reads per gate
-            q->u.assign(u.begin() + (size_t)i * kN, u.begin() + (size_t)(i + 1) * kN);
-        }
-        ms[4] += ms_since(t);
+    const int rc = tfhe_amd_internal_gate_batch_rows(l, gate, n, &res, in, mux ? 3 : 2, d_var);
+    ms[2] += ms_since(t);
+    for (int i = 0; i < n; ++i) {
+        Tier1Req *q = batch[i];
+        q->rc = rc;
+        if (rc != TFHE_AMD_OK) continue;
+        q->r->b = rr[i].b;
+        q->r->current_variance = rr[i].current_variance;
+        q->var_done = true;
     }
+    ms[4] += ms_since(t);
 }
 
 static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b, const LweSample *c,
@@ -1133,7 +1150,9 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
             l = e->qlane[li];
         }
         if (!l) die_dramatically("tfhe_amd: cannot create the Tier-1 queue's GPU lane");
-        run_tier1_batch(l, batch, bms);
+        const double *d_var = ks_variance_table(bk);
+        if (!d_var) die_dramatically("tfhe_amd: cannot upload the key-switching key's row variances");
+        run_tier1_batch(l, batch, bms, d_var);
         lk.lock();
         for (int k = 0; k < 5; ++k) q.ms[k] += bms[k];
         const int n = (int)batch.size();
@@ -1153,6 +1172,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     }
     // (otherwise: done by another thread's batch, whose leader did this call's bookkeeping)
     check(req.rc, "gate");
+    if (req.var_done) return;
     const Tier1Clock::time_point tv = Tier1Clock::now();
     r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
     q.var_ns += (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Tier1Clock::now() - tv).count();
@@ -1258,25 +1278,6 @@ int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, in
 // its pinned staging buffer and scatters the results back, pipelined in slices of one round, with
 // current_variance computed on the device (tfhe_amd_internal_gate_batch_rows).  result may be the
 // same array as an input.
-static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
-    // the KSK row variances on the device, once per key: each slice's current_variance is summed by
-    // k_ks_variance (the reference's order of double adds) instead of on the host from the slice's
-    // 4 KB-per-gate key-switch inputs (B = 1024: ~16 ms of host work and a 4 MB copy)
-    std::shared_ptr<KeyEntry> e = entry_for(bk->bkFFT, nullptr);
-    std::lock_guard<std::mutex> lk(e->mu);
-    if (!e->d_var) {
-        const LweKeySwitchKey *ks = bk->bkFFT->ks;
-        std::vector<double> var((size_t)kN * kKsT * kKsBase);
-        for (int i = 0; i < kN; ++i)
-            for (int j = 0; j < kKsT; ++j)
-                for (int h = 0; h < kKsBase; ++h)
-                    var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
-        void *dv = nullptr;
-        if (tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv)) return nullptr;
-        e->d_var = (double *)dv;
-    }
-    return e->d_var;
-}
 
 EXPORT int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
                                 const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk) {

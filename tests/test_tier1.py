@@ -142,9 +142,11 @@ def test_tier1_current_variance_as_reference(keyset, okey, rng):
 @pytest.mark.gpu
 def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
     """tfhe_amd_boots_batch over LweSample arrays (SURVEY.md §8(b)'s LweSample convenience overload):
-    1 100 NAND gates (two pipelined slices: 1 024 + 76) and 33 MUX gates give the Torus32 words of the
-    device batch path, also in place (result = the first input array), and current_variance — summed on the device by k_ks_variance in the reference's order
-    of double adds — equals, bit for bit, the Tier-1 gates' (summed on the host) on sampled rows."""
+    1 100 NAND gates (two pipelined slices: 1 024 + 76) and 33 MUX gates give the Torus32 words of
+    the device batch path, also in place (result = the first input array), and current_variance —
+    summed on the device by k_ks_variance in the reference's order of double adds — equals, bit for
+    bit, the single Tier-1 gates' on sampled rows (test_tier1_current_variance_as_reference pins
+    those to the reference's sum)."""
     import ctypes
     import time
     import numpy as np
