@@ -147,14 +147,10 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
-// PF (the paired kernel's one-wave-per-SIMD build, k_blind_rotate_v6p<1>): the key slices of step i
-// arrive in pre[0] (output 1 - w) and pre[1] (output w), loaded during step i - 1, and each is
-// reloaded with step i + 1's slice as soon as its MAC has consumed it, so every key load has a
-// whole step to land (64 more VGPRs live across the step: a 512-register, one-wave budget).
-template <int WAVES, bool RREG, bool RSW = false, bool PF = false>
+template <int WAVES, bool RREG, bool RSW = false>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
-                                        uint32_t &bad, Cx (&pre)[2][2][8] V6_STAMPS_PARAM) {
+                                        uint32_t &bad V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
@@ -269,25 +265,15 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     Cx Y[8];
     // (issuing them at the top of the step instead, in flight for the whole forward transform,
     // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
-    const double2 *bk_next = g.bk + ((size_t)(i + 1 < kn ? i + 1 : i) * 8 + (size_t)w * 4) * 512 + L;
-    if constexpr (PF) {
-        (void)bv;
-        fft_fwd_C<2>(D, tC);
-        mac6(D, pre[0], Y);
-        load_bk(pre[0], bk_next, KEYC(1 - w));   // step i + 1's first slice
-        __builtin_amdgcn_sched_barrier(0);
-    } else {
-        (void)bk_next;
-        load_bk(bv, bk, KEYC(1 - w));
-        __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
-        fft_fwd_C<2>(D, tC);
-        mac6(D, bv, Y);
-    }
+    // (a one-wave build of the paired kernel that loads each key slice a whole step ahead, 64 more
+    // VGPRs live across the step, measured slower: B = 512 2.336 vs 2.273 ms, profiles/r04f_*)
+    load_bk(bv, bk, KEYC(1 - w));
+    __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
+    fft_fwd_C<2>(D, tC);
+    mac6(D, bv, Y);
     V6_STAMP(2);
-    if constexpr (!PF) {
-        load_bk(bv, bk, KEYC(w));
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    load_bk(bv, bk, KEYC(w));
+    __builtin_amdgcn_sched_barrier(0);
 #ifndef TFHE_AMD_DIAG_NOHAND   // timing diagnostic (wrong results): no partial-sum hand-off
     store_C(X, Y, L);
 #endif
@@ -311,12 +297,7 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         // the partner's partial sum seeds the second MAC (16 fp64 fewer per wave-step: B = 1 / 256
         // / 512 / 1 024 / 4 096 -0.9 / -1.2 / -0.9 / -0.8 / -0.6 %, profiles/r03_seed_mac2_ab.txt,
         // r03_seed_mac2_latency_ab.txt)
-        if constexpr (PF) {
-            mac6_seeded(D, pre[1], o, Y);
-            load_bk(pre[1], bk_next, KEYC(w));   // step i + 1's second slice
-        } else {
-            mac6_seeded(D, bv, o, Y);
-        }
+        mac6_seeded(D, bv, o, Y);
     }
     pass_dit_C(Y);
     const Tw4 tB = TW7(tw7_invB);
@@ -414,7 +395,7 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 // the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
 // exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
 // computes but writes nothing.
-template <int WAVES, bool RREG, int C = 1, bool PF = false>
+template <int WAVES, bool RREG, int C = 1>
 __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
                                            bool live = true) {
@@ -468,13 +449,6 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
     uint32_t bad = 0;                    // some coefficient's round(4c) != 0 mod 4 (distance >= 1/8)
     int a_next = sh.bara[0];
     int own = w;                         // this wave's LDS buffer (the waves swap every step)
-    static_assert(!PF || C == 2, "key prefetch assumes no skipped steps");
-    Cx pre[2][2][8];                     // PF: the next step's key slices
-    if constexpr (PF) {
-        const double2 *bk0 = g.bk + (size_t)w * 4 * 512 + L;
-        load_bk(pre[0], bk0, 1 - w);
-        load_bk(pre[1], bk0, w);
-    }
     for (int i = 0; i < kn; ++i) {
         const int a = a_next;
         a_next = sh.bara[i + 1 < kn ? i + 1 : i];   // a step ahead: no LDS round trip at the loop head
@@ -488,8 +462,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG, RREG && C == 1, PF>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
-                                                 pre V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG, RREG && C == 1>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
 #if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
@@ -569,8 +542,7 @@ __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Ar
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES, true, 2, WAVES == 1>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct,
-                                           live);
+    br_v6_body<WAVES, true, 2>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
 template <int WAVES, bool RREG>
@@ -625,8 +597,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo, bad = 0;
         // RREG: the throughput launches' form (the scalar-branch permutation, RSW), so that the
         // forced rotation edges of test_register_rotation_edges reach it
-        Cx pre[2][2][8];
-        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, pre V6_STAMPS_ARG);
+        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -747,12 +718,6 @@ static bool v6_pair(const DeviceKey &key, long n) {
 }
 // the register / ds_bpermute rotation (cmux_v6 RREG) for launches of more than one workgroup
 // per CU; TFHE_AMD_V6_RREG=0/1 forces it off/on (experiments, tests)
-// The paired kernel's one-wave-per-SIMD build with a whole step of key prefetch (cmux_v6 PF,
-// k_blind_rotate_v6p<1>); TFHE_AMD_V6P_PF=0/1 (default: see below)
-static bool v6p_prefetch() {
-    static const char *env = getenv("TFHE_AMD_V6P_PF");
-    return env ? atoi(env) != 0 : false;
-}
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -787,15 +752,9 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
         const long n = total - base < chunk ? total - base : chunk;
         if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
-            if (v6p_prefetch()) {
-                trace_kernel("k_blind_rotate_v6p(paired+reg-rotation+key-prefetch)");
-                hipLaunchKernelGGL(k_blind_rotate_v6p<1>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
-            } else {
-                trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
-                hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
-            }
+            trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
+            hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                               v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
         } else {
             trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6(reg-rotation)" : "k_blind_rotate_v6(lds-rotation)");
             if (v6_rreg(key, n))

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <condition_variable>
@@ -875,6 +876,32 @@ static void host_copy(std::initializer_list<CopyJob> jobs) {
     HostCopyPool::get().copy(jobs.begin(), (int)jobs.size());
 }
 
+// TFHE_AMD_HOST_TRACE=1: one stderr line per host-pointer batch call with its host-side phases
+// (ms): staging copies, waits for the device, unstaging copies, the whole call
+struct HostTrace {
+    static bool on() {
+        static const bool v = [] {
+            const char *e = getenv("TFHE_AMD_HOST_TRACE");
+            return e && e[0] == '1';
+        }();
+        return v;
+    }
+    using clk = std::chrono::steady_clock;
+    clk::time_point t0 = clk::now(), t = t0;
+    double stage = 0, wait = 0, unstage = 0, issue = 0;
+    void lap(double &acc) {
+        if (!on()) return;
+        const clk::time_point n = clk::now();
+        acc += std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    }
+    void report(const char *what, int B) {
+        if (!on()) return;
+        fprintf(stderr, "host_trace %s B=%d stage=%.3f issue=%.3f wait=%.3f unstage=%.3f total=%.3f\n", what, B,
+                stage, issue, wait, unstage, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+    }
+};
+
 static int host_slice() {   // TFHE_AMD_HOST_SLICE overrides (0: one unsliced batch)
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_HOST_SLICE");
@@ -903,11 +930,15 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
     const size_t out0 = 3 * R * (size_t)B;
     const int S = host_slice();
     const int nsl = (B + S - 1) / S;
+    HostTrace tr;
     auto unstage = [&](int s) -> int {
         const int s0 = s * S, n = std::min(S, B - s0);
         const int32_t *ho = h + out0 + R * (size_t)s0;
+        tr.lap(tr.issue);
         HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
+        tr.lap(tr.wait);
         host_copy({{res_a + (size_t)s0 * kn, ho, (size_t)n * kn * 4}, {res_b + s0, ho + (size_t)n * kn, (size_t)n * 4}});
+        tr.lap(tr.unstage);
         return TFHE_AMD_OK;
     };
     for (int s = 0; s < nsl; ++s) {
@@ -920,7 +951,9 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
                 jobs.push_back({hi + k * na, in_a[k] + (size_t)s0 * kn, na * 4});
                 jobs.push_back({hi + nin * na + (size_t)k * n, in_b[k] + s0, (size_t)n * 4});
             }
+            tr.lap(tr.issue);
             HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+            tr.lap(tr.stage);
         }
         HIPCHK(hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in));
         HIPCHK(hipEventRecord(c->ev_in, c->copy_in));
@@ -938,7 +971,9 @@ static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *r
             if (r) return r;
         }
     }
-    return unstage(nsl - 1);
+    const int r = unstage(nsl - 1);
+    tr.report("sliced", B);
+    return r;
 }
 
 // Record batches (tfhe_api.cpp tfhe_amd_boots_batch over LweSample arrays).  The records' rows
@@ -999,10 +1034,13 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
     const int nsl = (B + S - 1) / S;
     const int halves = mux ? 2 : 1;
     std::vector<CopyJob> jobs;
+    HostTrace tr;
     auto scatter = [&](int s) -> int {
         const int s0 = s * S, n = std::min(S, B - s0);
         const int32_t *ho = h + out0 + R * (size_t)s0;
+        tr.lap(tr.issue);
         HIPCHK(hipEventSynchronize(c->ev_out[s & 1]));
+        tr.lap(tr.wait);
         jobs.clear();
         for (int i = 0; i < n; ++i) jobs.push_back({rec_a(*res, s0 + i), ho + (size_t)i * kn, (size_t)kn * 4});
         HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
@@ -1011,6 +1049,7 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
             rec_b(*res, s0 + i) = hb[i];
             rec_v(*res, s0 + i) = c->h_vout[s0 + i];
         }
+        tr.lap(tr.unstage);
         return TFHE_AMD_OK;
     };
     auto drain = [&] {
@@ -1024,9 +1063,11 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
         jobs.clear();
         for (int k = 0; k < nin; ++k)
             for (int i = 0; i < n; ++i) jobs.push_back({hi + k * na + (size_t)i * kn, rec_a(in[k], s0 + i), (size_t)kn * 4});
+        tr.lap(tr.issue);
         HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
         for (int k = 0; k < nin; ++k)
             for (int i = 0; i < n; ++i) hi[nin * na + (size_t)k * n + i] = rec_b(in[k], s0 + i);
+        tr.lap(tr.stage);
         hipError_t e = hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in);
         if (e == hipSuccess) e = hipEventRecord(c->ev_in, c->copy_in);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
@@ -1059,6 +1100,7 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
     }
     rc = scatter(nsl - 1);
     if (rc) drain();
+    tr.report("records", B);
     return rc;
 }
 
@@ -1103,13 +1145,16 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     const int nin = mux ? 3 : 2;
     const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
     int32_t *hb = h + nin * A, *db = d + nin * A;
+    HostTrace tr;
     {
         std::vector<CopyJob> jobs;
         for (int k = 0; k < nin; ++k) {
             jobs.push_back({h + k * A, in_a[k], A * 4});
             jobs.push_back({hb + (size_t)k * B, in_b[k], (size_t)B * 4});
         }
+        tr.lap(tr.issue);
         HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+        tr.lap(tr.stage);
     }
     HIPCHK(hipMemcpyAsync(d, h, (size_t)nin * (A + B) * 4, hipMemcpyHostToDevice, c->stream));
     int32_t *hr = h + 3 * (A + B), *dr = d + 3 * (A + B);
@@ -1117,8 +1162,12 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
                                  mux ? d + 2 * A : nullptr, mux ? db + 2 * B : nullptr, c->stream);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(hr, dr, (A + B) * 4, hipMemcpyDeviceToHost, c->stream));
+    tr.lap(tr.issue);
     HIPCHK(hipStreamSynchronize(c->stream));
+    tr.lap(tr.wait);
     host_copy({{res_a, hr, A * 4}, {res_b, hr + A, (size_t)B * 4}});
+    tr.lap(tr.unstage);
+    tr.report("unsliced", B);
     return TFHE_AMD_OK;
 }
 

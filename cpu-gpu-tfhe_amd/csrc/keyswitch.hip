@@ -601,17 +601,32 @@ hipError_t launch_ksk_to_v5(const int32_t *d_ksk, int32_t *d_ksk5, hipStream_t s
     return hipGetLastError();
 }
 
-// current_variance bookkeeping of B key-switched samples (tfhe_api.cpp tfhe_amd_boots_batch): per
-// sample the reference's sum over i < 1024, j < 8 of the variance of the key-switching-key row its
-// non-zero digit selects (lweKeySwitchTranslate_fromArray, lwe-keyswitch-functions.cu:101-127;
-// lwe-functions.cu:150), in the same i, j order with the same IEEE double adds, so the doubles
-// are the reference's.  One thread per sample (halves = 2: the MUX's u1 + u2).  var [1024][8][4].
+// current_variance bookkeeping of B key-switched samples (tfhe_api.cpp tfhe_amd_boots_batch and the
+// Tier-1 queue): per sample the reference's sum over i < 1024, j < 8 of the variance of the
+// key-switching-key row its non-zero digit selects (lweKeySwitchTranslate_fromArray,
+// lwe-keyswitch-functions.cu:101-127; lwe-functions.cu:150), in the same i, j order with the same
+// IEEE double adds, so the doubles are the reference's.  One thread per sample (halves = 2: the
+// MUX's u1 + u2).  var [1024][8][4], then var[kKsVarUniform] != 0 when every row has the same
+// variance (the reference's lweCreateKeySwitchKey encrypts every row with the same alpha): the sum
+// of k such adds is then table[k] = var[kKsVarUniform + 1 + k], built on the host in the same order,
+// and a sample needs only its count of non-zero digits.
 __global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ u_a, int B, int halves,
                                                     const double *__restrict__ var, double *__restrict__ out) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= B) return;
     const int32_t *u = u_a + (size_t)g * kN;
     const int32_t *u2 = halves == 2 ? u_a + ((size_t)B + g) * kN : u;
+    static_assert(kKsT * kKsBasebit == 16 && kKsBase == 4, "digit count below assumes 8 base-4 digits");
+    if (var[kKsVarUniform] != 0.0) {
+        int k = 0;
+#pragma unroll 8
+        for (int i = 0; i < kN; ++i) {
+            const uint32_t x = ((uint32_t)u[i] + (halves == 2 ? (uint32_t)u2[i] : 0u) + kKsPrecOffset) >> 16;
+            k += __builtin_popcount((x | (x >> 1)) & 0x5555u);   // non-zero 2-bit digits
+        }
+        out[g] = var[kKsVarUniform + 1 + k];
+        return;
+    }
     double v = 0.0;
     // 4 coefficients = 32 table reads in flight per round (a one-thread-per-sample sum is a chain
     // of dependent adds; its loads must not be): a zero digit reads entry 0 of its row and adds

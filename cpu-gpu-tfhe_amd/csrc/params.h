@@ -19,6 +19,10 @@ constexpr int kKsBasebit = 2;     // key-switch base 4
 constexpr int kKsBase = 1 << kKsBasebit;
 constexpr uint32_t kDecompOffset = 512u * ((1u << 22) + (1u << 12));   // 2149580800
 constexpr uint32_t kKsPrecOffset = 1u << (32 - (1 + kKsBasebit * kKsT)); // 2^15
+// current_variance tables (k_ks_variance): the KSK row variances [kN][kKsT][kKsBase], then a flag
+// (non-zero: every row has the same variance), then the sequential sums of k copies, k <= kN kKsT
+constexpr int kKsVarUniform = kN * kKsT * kKsBase;
+constexpr int kKsVarWords = kKsVarUniform + 1 + kN * kKsT + 1;
 
 // Device key-switch key rows: for each (i<1024, j<8) the three non-zero digits h=1..3,
 // each row = 500 a-coefficients, b, zero padding to 512 int32 (2 KB, 16-B aligned).

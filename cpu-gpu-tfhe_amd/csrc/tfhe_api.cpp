@@ -557,6 +557,10 @@ struct Tier1Req {
     std::mutex m;             // wake-up of the caller: done (its batch finished) or a call to lead
     std::condition_variable cv;
     bool signaled = false, done = false;
+    // a finished batch's callers are woken as a binary tree over wl: the leader wakes wl[0], wl[1],
+    // and the caller at wl[i] wakes wl[2i + 2], wl[2i + 3] (log2 depth instead of one by one)
+    std::shared_ptr<std::vector<Tier1Req *>> wl;
+    int wi = -1;
     void wake(bool finished) {   // the request may be gone once m is released with done set
         std::lock_guard<std::mutex> lk(m);
         done = done || finished;
@@ -949,11 +953,24 @@ static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
     std::lock_guard<std::mutex> lk(e->mu);
     if (!e->d_var) {
         const LweKeySwitchKey *ks = bk->bkFFT->ks;
-        std::vector<double> var((size_t)kN * kKsT * kKsBase);
+        std::vector<double> var(kKsVarWords, 0.0);
+        bool uniform = true;
+        const double v0 = ks->ks[0][0][1].current_variance;
         for (int i = 0; i < kN; ++i)
             for (int j = 0; j < kKsT; ++j)
-                for (int h = 0; h < kKsBase; ++h)
-                    var[((size_t)i * kKsT + j) * kKsBase + h] = ks->ks[i][j][h].current_variance;
+                for (int h = 0; h < kKsBase; ++h) {
+                    const double v = ks->ks[i][j][h].current_variance;
+                    var[((size_t)i * kKsT + j) * kKsBase + h] = v;
+                    if (h && memcmp(&v, &v0, sizeof v) != 0) uniform = false;   // rows a digit selects
+                }
+        if (uniform) {   // the sums of k equal terms, added one at a time as the reference does
+            var[kKsVarUniform] = 1.0;
+            double acc = 0.0;
+            for (int k = 0; k <= kN * kKsT; ++k) {
+                var[kKsVarUniform + 1 + k] = acc;
+                acc += v0;
+            }
+        }
         void *dv = nullptr;
         if (tfhe_amd_internal_upload(e->primary, var.data(), sizeof(double) * var.size(), &dv)) return nullptr;
         e->d_var = (double *)dv;
@@ -1167,10 +1184,19 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         q.arrive_cv.notify_all();   // a collecting leader's expected count changed
         appoint();                  // this lane is free again
         lk.unlock();
+        auto wl = std::make_shared<std::vector<Tier1Req *>>();
         for (Tier1Req *x : batch)
-            if (x != &req) x->wake(true);   // x may return (and its request vanish) from here on
+            if (x != &req) wl->push_back(x);
+        for (int i = 0; i < (int)wl->size(); ++i) {
+            (*wl)[i]->wl = wl;
+            (*wl)[i]->wi = i;
+        }
+        for (int i = 0; i < 2 && i < (int)wl->size(); ++i) (*wl)[i]->wake(true);   // may return from here on
+    } else {
+        // done by another thread's batch, whose leader did this call's bookkeeping: pass the wake-up on
+        const std::shared_ptr<std::vector<Tier1Req *>> wl = std::move(req.wl);
+        for (int c = 2 * req.wi + 2; wl && c < 2 * req.wi + 4 && c < (int)wl->size(); ++c) (*wl)[c]->wake(true);
     }
-    // (otherwise: done by another thread's batch, whose leader did this call's bookkeeping)
     check(req.rc, "gate");
     if (req.var_done) return;
     const Tier1Clock::time_point tv = Tier1Clock::now();
