@@ -140,6 +140,68 @@ def test_tier1_current_variance_as_reference(keyset, okey, rng):
 
 
 @pytest.mark.gpu
+def test_current_variance_nonuniform_key_rows(rng):
+    """The device-side current_variance sum has two forms (keyswitch.hip k_ks_variance): a table of
+    the sequential sums of k equal terms when every key-switching-key row carries the same variance
+    (the reference's lweCreateKeySwitchKey), and the full sequential sum otherwise.  A key whose row
+    variances are made unequal before its first gate takes the second form; bootsNAND (Tier-1 queue)
+    and tfhe_amd_boots_batch (record path, 3 gates) must still give the reference's double exactly."""
+    import ctypes
+    import numpy as np
+    import oracle_ctypes as O
+    import tfhe_amd as T
+
+    class LweSample(ctypes.Structure):
+        _fields_ = [("a", ctypes.POINTER(ctypes.c_int32)), ("b", ctypes.c_int32), ("current_variance", ctypes.c_double)]
+    P = ctypes.c_void_p
+    lib = T.lib
+    lib.bootsNAND.argtypes = [P, P, P, P]
+    lib.tfhe_amd_boots_batch.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P]
+    K = T.SecretKeyset(seed=(27, 18, 28))
+    ok = O.OracleKey(K.bk, K.ksk, use_ntt=True)
+    try:
+        cloud = K.cloud
+        bkfft = P.from_address(cloud + 16).value
+        ks = P.from_address(bkfft + 40).value
+        rows = (LweSample * (1024 * 8 * 4)).from_address(P.from_address(ks + 24).value)
+        for r in range(1024 * 8 * 4):   # unequal rows, before the key's device tables exist
+            rows[r].current_variance *= 1.0 + ((r * 37) % 11) * 1e-3
+        row_var = np.array([rows[r].current_variance for r in range(1024 * 8 * 4)])
+
+        def expected(u):
+            v = 0.0
+            for i in range(1024):
+                aibar = (int(u[i]) + (1 << 15)) & 0xFFFFFFFF
+                for j in range(8):
+                    aij = (aibar >> (30 - 2 * j)) & 3
+                    if aij:
+                        v += row_var[(i * 8 + j) * 4 + aij]
+            return v
+
+        B = 3
+        arrs = [lib.new_gate_bootstrapping_ciphertext_array(B, P(K.params)) for _ in range(3)]
+        s = [(LweSample * B).from_address(p) for p in arrs]
+        enc = [K.encrypt(rng.integers(0, 2, B), rng) for _ in range(2)]
+        for k in range(2):
+            for i in range(B):
+                ctypes.memmove(s[k][i].a, enc[k][0][i].ctypes.data, 4 * 500)
+                s[k][i].b = int(enc[k][1][i])
+        t_a = (-(enc[0][0].astype(np.int64)) - enc[1][0]).astype(np.int64)
+        t_b = np.int64(1 << 29) - enc[0][1].astype(np.int64) - enc[1][1]
+        u_a, _ = ok.woks_batch(1 << 29, t_a, t_b)
+        lib.bootsNAND(P(ctypes.addressof(s[2][0])), P(ctypes.addressof(s[0][0])), P(ctypes.addressof(s[1][0])), P(cloud))
+        assert s[2][0].current_variance == expected(u_a[0]) > 0
+        assert lib.tfhe_amd_boots_batch(T.GATES["NAND"], P(arrs[2]), P(arrs[0]), P(arrs[1]), None, B, P(cloud)) == 0
+        for i in range(B):
+            assert s[2][i].current_variance == expected(u_a[i]), i
+        for p in arrs:
+            lib.delete_gate_bootstrapping_ciphertext_array(B, P(p))
+    finally:
+        del ok
+        K.close()
+
+
+@pytest.mark.gpu
 def test_boots_batch_lwesample_arrays(keyset, ctx, rng):
     """tfhe_amd_boots_batch over LweSample arrays (SURVEY.md §8(b)'s LweSample convenience overload):
     1 100 NAND gates (two pipelined slices: 1 024 + 76) and 33 MUX gates give the Torus32 words of
