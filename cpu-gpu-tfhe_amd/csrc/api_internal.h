@@ -59,6 +59,8 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
 int tfhe_amd_internal_upload(TfheAmdContext *c, const void *host, size_t bytes, void **dev);
 void tfhe_amd_internal_free(int device, void *dev);
 int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const double *d_var, double *out);
+// the same for the context's last mixed-gate batch (gate i's variance in out[i])
+int tfhe_amd_internal_mixed_variance(TfheAmdContext *c, int B, const double *d_var, double *out);
 // Rows of an array of records that each point to their a[500] and hold b (and current_variance):
 // record i is at base + i * stride; its a pointer at a_off, b at b_off, current_variance at v_off
 // (tfhe_api.cpp: LweSample arrays, without the engine knowing the struct)

@@ -193,6 +193,7 @@ struct TfheAmdContext {
     std::string last_kernels;   // kernels of the last batch entry point (tfhe_amd_last_kernels)
     void *mtab = nullptr;       // mixed-gate batches: device row / key-switch tables
     size_t mtab_bytes = 0;
+    int mtab_rows = 0;          // rows of the last mixed-gate batch (its key-switch table follows them)
 };
 
 // Collects the launches of one C-ABI batch call into its context's last_kernels; nested calls
@@ -1240,6 +1241,7 @@ extern "C" int tfhe_amd_gate_batch_mixed_host(TfheAmdContext *c, int B, const in
     HIPCHK(hipMemcpyAsync(d + WA, h + WA, (size_t)3 * B * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->mtab, rw.data(), sizeof(CircRow) * rw.size(), hipMemcpyHostToDevice, s));
     const CircKs *d_ks = (const CircKs *)((char *)c->mtab + sizeof(CircRow) * rw.size());
+    c->mtab_rows = rows;
     HIPCHK(hipMemcpyAsync((void *)d_ks, ks.data(), sizeof(CircKs) * ks.size(), hipMemcpyHostToDevice, s));
     {
         ProfScope ps(c, s, true);
@@ -1362,6 +1364,32 @@ int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const do
     HIPCHK(launch_ks_variance(c->u_a, B, halves, d_var, d_out, c->stream));
     HIPCHK(hipMemcpyAsync(out, d_out, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return TFHE_AMD_OK;
+}
+
+// current_variance of the context's last mixed-gate batch (tfhe_amd_gate_batch_mixed_host: its row and
+// key-switch tables and extracted samples are still in the scratch), on the device, into out [B]
+int tfhe_amd_internal_mixed_variance(TfheAmdContext *c, int B, const double *d_var, double *out) {
+    if (!c || B <= 0 || !d_var || !out || !c->mtab || c->mtab_rows < B) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceScope dev_scope(c->device);
+    HIPCHK(dev_scope.rc);
+    if (B > c->vcap) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_vout) (void)hipHostFree(c->h_vout);
+        if (c->d_vout) (void)hipFree(c->d_vout);
+        c->h_vout = nullptr;
+        c->d_vout = nullptr;
+        c->vcap = 0;
+        HIPCHK(hipMalloc(&c->d_vout, sizeof(double) * (size_t)c->cap));
+        HIPCHK(hipHostMalloc(&c->h_vout, sizeof(double) * (size_t)c->cap, hipHostMallocDefault));
+        c->vcap = c->cap;
+    }
+    const CircKs *d_ks = (const CircKs *)((char *)c->mtab + sizeof(CircRow) * (size_t)c->mtab_rows);
+    HIPCHK(launch_ks_variance_rows(c->u_a, B, d_ks, d_var, c->d_vout, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_vout, c->d_vout, sizeof(double) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(out, c->h_vout, sizeof(double) * (size_t)B);
     return TFHE_AMD_OK;
 }
 

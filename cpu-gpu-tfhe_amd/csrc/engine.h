@@ -166,6 +166,8 @@ hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s
 // current_variance of B key-switched samples u (halves = 2: u1 + u2) from the key-switching key's
 // row variances var [kN][kKsT][kKsBase] (reference order of the double adds), into out [B]
 hipError_t launch_ks_variance(const int32_t *u_a, int B, int halves, const double *var, double *out, hipStream_t s);
+hipError_t launch_ks_variance_rows(const int32_t *u_a, int B, const CircKs *ks, const double *var, double *out,
+                                   hipStream_t s);
 // Key switch of u (+ u2 if non-null) + (0, add_b) -> res (n=500).
 hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,
                             const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,

@@ -610,22 +610,17 @@ hipError_t launch_ksk_to_v5(const int32_t *d_ksk, int32_t *d_ksk5, hipStream_t s
 // variance (the reference's lweCreateKeySwitchKey encrypts every row with the same alpha): the sum
 // of k such adds is then table[k] = var[kKsVarUniform + 1 + k], built on the host in the same order,
 // and a sample needs only its count of non-zero digits.
-__global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ u_a, int B, int halves,
-                                                    const double *__restrict__ var, double *__restrict__ out) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= B) return;
-    const int32_t *u = u_a + (size_t)g * kN;
-    const int32_t *u2 = halves == 2 ? u_a + ((size_t)B + g) * kN : u;
+__device__ __forceinline__ double ks_var_one(const int32_t *__restrict__ u, const int32_t *__restrict__ u2,
+                                             const double *__restrict__ var) {
     static_assert(kKsT * kKsBasebit == 16 && kKsBase == 4, "digit count below assumes 8 base-4 digits");
     if (var[kKsVarUniform] != 0.0) {
         int k = 0;
 #pragma unroll 8
         for (int i = 0; i < kN; ++i) {
-            const uint32_t x = ((uint32_t)u[i] + (halves == 2 ? (uint32_t)u2[i] : 0u) + kKsPrecOffset) >> 16;
+            const uint32_t x = ((uint32_t)u[i] + (u2 ? (uint32_t)u2[i] : 0u) + kKsPrecOffset) >> 16;
             k += __builtin_popcount((x | (x >> 1)) & 0x5555u);   // non-zero 2-bit digits
         }
-        out[g] = var[kKsVarUniform + 1 + k];
-        return;
+        return var[kKsVarUniform + 1 + k];
     }
     double v = 0.0;
     // 4 coefficients = 32 table reads in flight per round (a one-thread-per-sample sum is a chain
@@ -635,8 +630,7 @@ __global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ 
     for (int i0 = 0; i0 < kN; i0 += U) {
         uint32_t ab[U];
 #pragma unroll
-        for (int k = 0; k < U; ++k)
-            ab[k] = (uint32_t)u[i0 + k] + (halves == 2 ? (uint32_t)u2[i0 + k] : 0u) + kKsPrecOffset;
+        for (int k = 0; k < U; ++k) ab[k] = (uint32_t)u[i0 + k] + (u2 ? (uint32_t)u2[i0 + k] : 0u) + kKsPrecOffset;
         double t[U][kKsT];
 #pragma unroll
         for (int k = 0; k < U; ++k)
@@ -653,7 +647,32 @@ __global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ 
                 v = __dadd_rn(v, aij ? t[k][j] : 0.0);
             }
     }
-    out[g] = v;
+    return v;
+}
+
+__global__ __launch_bounds__(64) void k_ks_variance(const int32_t *__restrict__ u_a, int B, int halves,
+                                                    const double *__restrict__ var, double *__restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B) return;
+    out[g] = ks_var_one(u_a + (size_t)g * kN, halves == 2 ? u_a + ((size_t)B + g) * kN : nullptr, var);
+}
+
+// the same for a mixed-kind batch (tfhe_amd_gate_batch_mixed_host): gate g's key-switch input is
+// extracted row ks[g].r1 (+ row ks[g].r2 for a MUX)
+__global__ __launch_bounds__(64) void k_ks_variance_rows(const int32_t *__restrict__ u_a, int B,
+                                                         const CircKs *__restrict__ ks, const double *__restrict__ var,
+                                                         double *__restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B) return;
+    const CircKs k = ks[g];
+    out[g] = ks_var_one(u_a + (size_t)k.r1 * kN, k.r2 >= 0 ? u_a + (size_t)k.r2 * kN : nullptr, var);
+}
+
+hipError_t launch_ks_variance_rows(const int32_t *u_a, int B, const CircKs *ks, const double *var, double *out,
+                                   hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ks_variance_rows, dim3((B + 63) / 64), dim3(64), 0, s, u_a, B, ks, var, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_ks_variance(const int32_t *u_a, int B, int halves, const double *var, double *out, hipStream_t s) {

@@ -551,9 +551,8 @@ struct Tier1Req {
     LweSample *r;
     const LweSample *a, *b, *c;
     bool taken = false;   // in a running batch (queue lock)
-    bool var_done = false;   // its batch wrote r->current_variance (device-side sum)
+
     int rc = TFHE_AMD_OK;
-    std::vector<int32_t> u;   // its key-switch input: the caller derives current_variance from it
     std::mutex m;             // wake-up of the caller: done (its batch finished) or a call to lead
     std::condition_variable cv;
     bool signaled = false, done = false;
@@ -602,9 +601,9 @@ struct Coalescer {
     long long batches = 0, gates = 0, largest = 0, overlapped = 0;
     // where a batch's time goes (ms, summed over batches; tfhe_amd_tier1_queue_times):
     // 0 the leader's straggler wait, 1 packing, 2 the device gate batch (staging, copies, kernels,
-    // synchronize), 3 the key-switch inputs' readback, 4 unpacking, 5 the callers' variance sums
+    // synchronize), 3 the current_variance sums on the device (mixed kinds; single-kind batches
+    // sum them inside 2), 4 unpacking
     double ms[5] = {0, 0, 0, 0, 0};
-    std::atomic<long long> var_ns{0};   // phase 5, added without the queue's lock
 };
 
 struct KeyEntry {
@@ -991,49 +990,43 @@ static double ms_since(Tier1Clock::time_point &t) {
     return d;
 }
 
-static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms) {
+static void run_tier1_mixed(TfheAmdContext *l, const std::vector<Tier1Req *> &batch, double *ms,
+                            const double *d_var) {
     Tier1Clock::time_point t = Tier1Clock::now();
-    std::vector<int32_t> buf, u;
+    std::vector<int32_t> buf;
     std::vector<int> gates;
+    std::vector<double> var;
     const int total = (int)batch.size();
     for (int s0 = 0; s0 < total; s0 += 512) {
         const int n = std::min(512, total - s0);
         const size_t A = (size_t)n * kn;
-        buf.assign(4 * A + 4 * (size_t)n, 0);
+        buf.resize(4 * A + 4 * (size_t)n);   // every word the launch reads is written below
         int32_t *aa = buf.data(), *ba = aa + A, *ca = ba + A, *ra = ca + A;
         int32_t *ab = ra + A, *bb = ab + n, *cb = bb + n, *rb = cb + n;
         gates.resize(n);
-        int rows = 0;
         for (int i = 0; i < n; ++i) {
             const Tier1Req *q = batch[s0 + i];
             gates[i] = q->gate;
             memcpy(aa + (size_t)i * kn, q->a->a, kn * 4); ab[i] = q->a->b;
             memcpy(ba + (size_t)i * kn, q->b->a, kn * 4); bb[i] = q->b->b;
             if (q->gate == TFHE_GATE_MUX) { memcpy(ca + (size_t)i * kn, q->c->a, kn * 4); cb[i] = q->c->b; }
-            rows += q->gate == TFHE_GATE_MUX ? 2 : 1;
         }
         ms[1] += ms_since(t);
-        const int rc = tfhe_amd_gate_batch_mixed_host(l, n, gates.data(), ra, rb, aa, ab, ba, bb, ca, cb);
+        int rc = tfhe_amd_gate_batch_mixed_host(l, n, gates.data(), ra, rb, aa, ab, ba, bb, ca, cb);
         ms[2] += ms_since(t);
+        // current_variance on the device from the launch's own key-switch table (a MUX's u1 + u2)
+        var.resize(n);
+        if (rc == TFHE_AMD_OK) rc = tfhe_amd_internal_mixed_variance(l, n, d_var, var.data());
+        ms[3] += ms_since(t);
         if (rc != TFHE_AMD_OK) {
             for (int i = s0; i < total; ++i) batch[i]->rc = rc;
             return;
         }
-        u.resize((size_t)rows * kN);
-        check(tfhe_amd_internal_last_extracted(l, rows, 1, u.data()), "variance bookkeeping");
-        ms[3] += ms_since(t);
-        for (int i = 0, r = 0; i < n; ++i) {   // rows in request order: a MUX has two (u1 + u2)
+        for (int i = 0; i < n; ++i) {
             Tier1Req *q = batch[s0 + i];
             memcpy(q->r->a, ra + (size_t)i * kn, kn * 4);
             q->r->b = rb[i];
-            q->u.assign(u.begin() + (size_t)r * kN, u.begin() + (size_t)(r + 1) * kN);
-            if (q->gate == TFHE_GATE_MUX) {
-                for (int j = 0; j < kN; ++j)
-                    q->u[j] = (int32_t)((uint32_t)q->u[j] + (uint32_t)u[(size_t)(r + 1) * kN + j]);
-                r += 2;
-            } else {
-                r += 1;
-            }
+            q->r->current_variance = var[i];
         }
         ms[4] += ms_since(t);
     }
@@ -1047,7 +1040,7 @@ static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
                             const double *d_var) {
     for (const Tier1Req *q : batch)
         if (q->gate != batch[0]->gate) {
-            run_tier1_mixed(l, batch, ms);
+            run_tier1_mixed(l, batch, ms, d_var);
             return;
         }
     Tier1Clock::time_point t = Tier1Clock::now();
@@ -1078,7 +1071,6 @@ static void run_tier1_batch(TfheAmdContext *l, const std::vector<Tier1Req *> &ba
         if (rc != TFHE_AMD_OK) continue;
         q->r->b = rr[i].b;
         q->r->current_variance = rr[i].current_variance;
-        q->var_done = true;
     }
     ms[4] += ms_since(t);
 }
@@ -1197,11 +1189,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         const std::shared_ptr<std::vector<Tier1Req *>> wl = std::move(req.wl);
         for (int c = 2 * req.wi + 2; wl && c < 2 * req.wi + 4 && c < (int)wl->size(); ++c) (*wl)[c]->wake(true);
     }
-    check(req.rc, "gate");
-    if (req.var_done) return;
-    const Tier1Clock::time_point tv = Tier1Clock::now();
-    r->current_variance = ks_variance(bk->bkFFT->ks, req.u.data());
-    q.var_ns += (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Tier1Clock::now() - tv).count();
+    check(req.rc, "gate");   // result and current_variance were written by the batch
 }
 
 // Builds the key's Tier-1 device context (key upload + conversion, HIP initialisation, the
@@ -1251,7 +1239,7 @@ EXPORT int tfhe_amd_tier1_queue_times(const TFheGateBootstrappingCloudKeySet *bk
             m[k] = e->q.ms[k];
             if (reset) e->q.ms[k] = 0;
         }
-        m[5] = 1e-6 * (double)(reset ? e->q.var_ns.exchange(0) : e->q.var_ns.load());
+        m[5] = 0.0;   // (the callers no longer sum current_variance themselves)
     }
     if (ms)
         for (int k = 0; k < 6; ++k) ms[k] = m[k];

@@ -224,8 +224,8 @@ int tfhe_amd_tier1_queue_stats(const TFheGateBootstrappingCloudKeySet *bk, long 
                                long long *largest, int reset);
 /* Where the queue's time went, in ms summed over its batches since the last reset: ms[0] the
  * leaders' straggler waits, [1] packing the requests, [2] the device gate batches (staging, copies,
- * kernels, synchronize), [3] reading back the key-switch inputs, [4] unpacking, [5] the callers'
- * current_variance sums (summed over callers, off the queue's critical path). */
+ * kernels incl. the current_variance sums of single-kind batches, synchronize), [3] the device
+ * current_variance sums of mixed-kind batches, [4] unpacking, [5] 0 (reserved). */
 int tfhe_amd_tier1_queue_times(const TFheGateBootstrappingCloudKeySet *bk, double ms[6], int reset);
 /* Build the key's Tier-1 device context now (HIP initialisation, key upload and conversion on the
  * device, the queue's stream and scratch: 0.1-0.3 s once per process and key) instead of inside

@@ -90,9 +90,9 @@ int main(int argc, char **argv) {
         snprintf(line, sizeof line,
                  "%s{\"threads\": %d, \"gates\": %d, \"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, "
                  "\"batches\": %lld, \"mean_batch\": %.2f, \"largest_batch\": %lld, \"ms_per_batch\": {\"wait\": %.3f, "
-                 "\"pack\": %.3f, \"device\": %.3f, \"readback\": %.3f, \"unpack\": %.3f, \"variance_per_caller\": %.4f}}",
+                 "\"pack\": %.3f, \"device\": %.3f, \"mixed_variance\": %.3f, \"unpack\": %.3f}}",
                  runs.empty() ? "" : ", ", T, n, dt, n / dt, bad, nb, nb ? (double)ng / nb : 0.0, big, qms[0] * pb,
-                 qms[1] * pb, qms[2] * pb, qms[3] * pb, qms[4] * pb, ng ? qms[5] / ng : 0.0);
+                 qms[1] * pb, qms[2] * pb, qms[3] * pb, qms[4] * pb);
         runs += line;
     }
     // mixed kinds: gate i is kind i mod 11 (the 10 binary gates and MUX), as threads of a real
@@ -109,6 +109,7 @@ int main(int argc, char **argv) {
     const int T = maxT, n = maxT * per_thread;
     for (int i = 0; i < n; i++) lweCopy(&out[i], &a[i], lp);
     tfhe_amd_tier1_queue_stats(bk, nullptr, nullptr, nullptr, 1);
+    tfhe_amd_tier1_queue_times(bk, nullptr, 1);
     t0 = omp_get_wtime();
 #pragma omp parallel for num_threads(T) schedule(static)
     for (int i = 0; i < n; i++) {
@@ -118,15 +119,20 @@ int main(int argc, char **argv) {
     const double dt_mixed = omp_get_wtime() - t0;
     long long nbm = 0, ngm = 0, bigm = 0;
     tfhe_amd_tier1_queue_stats(bk, &nbm, &ngm, &bigm, 1);
+    double mms[6];
+    tfhe_amd_tier1_queue_times(bk, mms, 1);
+    const double pbm = nbm ? 1.0 / nbm : 0.0;
     int bad_mixed = 0;
     for (int i = 0; i < n; i++) bad_mixed += !same(&out[i], &seq[i], dim);
     mismatches += bad_mixed;
     const char *co = getenv("TFHE_AMD_TIER1_COALESCE");
     printf("{\"coalesce\": %s, \"pool\": %d, \"sequential_gates_per_s\": %.1f, \"truth_errors\": %d, "
            "\"mismatches\": %d, \"runs\": [%s], \"mixed_kinds\": {\"threads\": %d, \"gates\": %d, "
-           "\"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, \"batches\": %lld, \"mean_batch\": %.2f}}\n",
+           "\"seconds\": %.4f, \"gates_per_s\": %.1f, \"mismatches\": %d, \"batches\": %lld, \"mean_batch\": %.2f, "
+           "\"ms_per_batch\": {\"wait\": %.3f, \"pack\": %.3f, \"device\": %.3f, \"mixed_variance\": %.3f, \"unpack\": %.3f}}}\n",
            co && co[0] == '0' ? "false" : "true", P, P / seq_s, truth_errors, mismatches, runs.c_str(), T, n,
-           dt_mixed, n / dt_mixed, bad_mixed, nbm, nbm ? (double)ngm / nbm : 0.0);
+           dt_mixed, n / dt_mixed, bad_mixed, nbm, nbm ? (double)ngm / nbm : 0.0, mms[0] * pbm, mms[1] * pbm,
+           mms[2] * pbm, mms[3] * pbm, mms[4] * pbm);
     delete_gate_bootstrapping_ciphertext_array(P, out);
     delete_gate_bootstrapping_ciphertext_array(P, seq);
     delete_gate_bootstrapping_ciphertext_array(P, b);

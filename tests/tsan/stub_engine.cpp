@@ -27,6 +27,7 @@ struct TfheAmdContext {
     std::recursive_mutex mu;
     std::vector<int32_t> last_u;   // the last batch's "extracted samples" [rows][kN]
     int last_rows = 0;
+    std::vector<char> last_mux;    // mixed batches: gate i is a MUX (two rows)
 };
 
 static std::atomic<uint64_t> g_uid{1};
@@ -151,6 +152,8 @@ static int rows_batch(TfheAmdContext *c, int n, const int *gates, int gate, int3
     if (gates) {   // mixed: rows in request order
         c->last_u.swap(u);
         c->last_rows = rows;
+        c->last_mux.assign(n, 0);
+        for (int i = 0; i < n; ++i) c->last_mux[i] = gates[i] == TFHE_GATE_MUX;
     } else {       // gate batch: halves x B, MUX halves apart
         std::vector<int32_t> h((size_t)rows * kN);
         const int halves = gate == TFHE_GATE_MUX ? 2 : 1;
@@ -272,6 +275,30 @@ int tfhe_amd_internal_ks_variance(TfheAmdContext *c, int B, int halves, const do
     }
     return TFHE_AMD_OK;
 }
+static double var_sum(const int32_t *u, const int32_t *u2, const double *var) {
+    double v = 0.;
+    for (int k = 0; k < kN; ++k) {
+        const uint32_t aibar = (uint32_t)u[k] + (u2 ? (uint32_t)u2[k] : 0u) + kKsPrecOffset;
+        for (int j = 0; j < kKsT; ++j) {
+            const uint32_t aij = (aibar >> (32 - (j + 1) * kKsBasebit)) & (kKsBase - 1);
+            if (aij) v += var[((size_t)k * kKsT + j) * kKsBase + aij];
+        }
+    }
+    return v;
+}
+// the last mixed batch's variances (rows in request order, a MUX's two rows summed)
+int tfhe_amd_internal_mixed_variance(TfheAmdContext *c, int B, const double *var, double *out) {
+    if (!c || B <= 0 || !var || !out) return TFHE_AMD_E_ARG;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if ((int)c->last_mux.size() < B) return TFHE_AMD_E_ARG;
+    for (int i = 0, r = 0; i < B; ++i) {
+        const bool mux = c->last_mux[i];
+        out[i] = var_sum(&c->last_u[(size_t)r * kN], mux ? &c->last_u[(size_t)(r + 1) * kN] : nullptr, var);
+        r += mux ? 2 : 1;
+    }
+    return TFHE_AMD_OK;
+}
+
 // record batches (tfhe_amd_boots_batch): gather, the stand-in batch, variance, scatter, in slices
 int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const TfheAmdRows *res,
                                       const TfheAmdRows *in, int nin, const double *d_var) {
