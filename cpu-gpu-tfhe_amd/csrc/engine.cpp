@@ -1069,9 +1069,11 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
         for (int k = 0; k < nin; ++k)
             for (int i = 0; i < n; ++i) hi[nin * na + (size_t)k * n + i] = rec_b(in[k], s0 + i);
         tr.lap(tr.stage);
-        hipError_t e = hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, c->copy_in);
-        if (e == hipSuccess) e = hipEventRecord(c->ev_in, c->copy_in);
-        if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+        // one slice: the copy in on the compute stream itself (no cross-stream event on the latency path)
+        hipStream_t cin = nsl > 1 ? c->copy_in : c->stream;
+        hipError_t e = hipMemcpyAsync(di, hi, R * (size_t)nin * n * 4, hipMemcpyHostToDevice, cin);
+        if (e == hipSuccess && nsl > 1) e = hipEventRecord(c->ev_in, c->copy_in);
+        if (e == hipSuccess && nsl > 1) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
         if (e != hipSuccess) {
             drain();
             HIPCHK(e);

@@ -578,7 +578,8 @@ struct Tier1Req {
 // that lane — one gate kind as a gate batch, several kinds as one mixed launch per 512 gates.
 // Two lanes (own stream + scratch each) alternate, so batch k + 1 is staged and launched while
 // batch k is still on the GPU or being unstaged: the queue no longer serialises a whole batch's
-// host work with the next one.  A lone thread is its own leader at once (B = 1 latency).  Callers
+// host work with the next one — once the two together exceed one ciphertext per CU; below that
+// the next leader waits for the running batch and merges its callers' next gates into one launch.  A lone thread is its own leader at once (B = 1 latency).  Callers
 // sleep on their own request: a finished batch's leader does its callers' bookkeeping and wakes
 // exactly them, and a freed lane wakes the oldest pending caller to lead (no wake-up of every
 // thread in the call per batch, which serialised 64 threads on the queue lock).
@@ -586,6 +587,7 @@ struct Tier1Req {
 // follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
 // shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [20, 1000] us.
 constexpr int kQueueLanes = 2;
+constexpr int kQueueMergeLimit = 256;   // gates two lanes' batches may hold together and still merge (MI355X CUs)
 struct Coalescer {
     std::mutex mu;
     std::condition_variable arrive_cv;   // a collecting leader waits here for stragglers
@@ -1130,6 +1132,15 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         // batches instead of one batch of T
         auto all_in = [&] { return (int)q.pending.size() >= q.inside - q.in_flight + q.returning; };
         double bms[5] = {0, 0, 0, 0, 0};
+        // merge instead of overlap: while the other lane's batch runs and both together would still
+        // hold at most one ciphertext per CU, a second launch beside it only shares its CUs (two
+        // latency-class launches of 31 run 2.15 ms each; one of 62 about 1.8), so wait for that batch
+        // and take its callers' next gates too
+        if (q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= kQueueMergeLimit) {
+            const auto t0 = std::chrono::steady_clock::now();
+            q.arrive_cv.wait(lk, [&] { return q.in_flight == 0; });
+            bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
         if (!all_in() && q.window_us > 0) {
             const auto t0 = std::chrono::steady_clock::now();
             const bool ok = q.arrive_cv.wait_for(lk, std::chrono::duration<double, std::micro>(q.window_us), all_in);
@@ -1141,7 +1152,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
                 q.window_us = std::max(20.0, 0.75 * q.window_us);
                 q.returning = 0;   // the released callers did not come back: stop expecting them
             }
-            bms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         }
         q.collecting = false;
         std::vector<Tier1Req *> batch;
