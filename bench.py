@@ -23,8 +23,11 @@ Rank 0 prints ONE JSON line.  Extra objects:
                  fp64 fraction at that clock.  `sustained` = the fp64 FMA rate the chip holds
                  under its power limit (tfhe_amd_fp64_ceiling: pure register FMA chains, at the
                  kernel's 2 waves per SIMD and at 8) and the kernel's fraction of each.
-  batches      : the same step at B = 1 and 4096 per GPU (BASELINE metric's other batch sizes)
+  batches      : the same step at B = 1, 512 and 4096 per GPU (BASELINE metric's other batch
+                 sizes; 512 = the per-GPU shape of the strong-scaled 4096 at N = 8)
   strong       : global batch 4096 split over the ranks (BASELINE: batch 4096 on 1..8 GPUs)
+  host_path    : (1 rank) the host-pointer API at B = 1024 and 4096: inputs and results in host
+                 memory, PCIe-inclusive, median call — for comparison, never `value`
   cpu_baseline : the optimized CPU port (oracle/cpu_fft.c: fp64 FFT external product, the
                  spqlios algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to
                  the exact oracle) timed on this host's cores on a bounded sample (rank 0, N=1),
@@ -70,6 +73,8 @@ def parse():
     ap.add_argument("--gate", default="NAND")
     ap.add_argument("--extra-batches", default="1,512,4096", help="per-GPU batch sizes also timed ('none' = none)")
     ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
+    ap.add_argument("--host-batches", default="1024,4096",
+                    help="PCIe-inclusive host-pointer path also timed at these batches (rank 0 of a 1-rank run; 'none')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the sustained fp64 ceiling measurement")
@@ -545,6 +550,26 @@ def main():
         line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
                           "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
                           "steps": steps, "truth_table_ok": ok}
+
+    # the host-pointer API (tfhe_amd_gate_batch_host: inputs and results in host memory, staged
+    # through pinned buffers, slices of 1 024 pipelined): PCIe-inclusive, never `value`
+    if world == 1 and args.host_batches not in ("none", "", "''"):
+        hp = {}
+        for s_ in args.host_batches.split(","):
+            b = int(s_)
+            x, y, dev, r_a, r_b, host_in = make_batch(b)
+            out = (np.zeros((b, 500), np.int32), np.zeros(b, np.int32))
+            ts = []
+            for k in range(7):
+                t0 = time.perf_counter()
+                ctx.gate_host(args.gate, *host_in, out=out)
+                if k >= 2:   # the first calls size the staging and warm the copy threads
+                    ts.append(time.perf_counter() - t0)
+            ms = float(np.median(ts)) * 1e3
+            ok = bool(np.array_equal(K.decrypt(*out), 1 - (x & y))) if args.gate == "NAND" else None
+            hp[str(b)] = {"value": b / ms * 1e3, "ms_per_call": ms, "calls": len(ts), "statistic": "median",
+                          "truth_table_ok": ok}
+        line["host_path"] = hp
 
     # one process driving every visible GPU through the library (tfhe_amd_multi_gate_batch_dev:
     # device-resident shards, one key replica per device, no collective) — what a C++ host such as

@@ -585,9 +585,13 @@ struct Tier1Req {
 // thread in the call per batch, which serialised 64 threads on the queue lock).
 // The window adapts to the callers: it starts at TFHE_AMD_TIER1_WINDOW_US (default 200 us),
 // follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
-// shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [20, 1000] us.
+// shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [200, 1000] us.
 constexpr int kQueueLanes = 2;
 constexpr int kQueueMergeLimit = 256;   // gates two lanes' batches may hold together and still merge (MI355X CUs)
+// the straggler window never drops below this: released callers come back within ~0.1 ms, and a
+// window that times out on them splits a team into partial batches (which then queue behind each
+// other); a caller that does not come back costs one such wait, after which it is no longer expected
+constexpr double kWindowFloorUs = 200.0;
 struct Coalescer {
     std::mutex mu;
     std::condition_variable arrive_cv;   // a collecting leader waits here for stragglers
@@ -938,6 +942,14 @@ static bool coalesce_enabled() {
     }();
     return on;
 }
+// TFHE_AMD_TIER1_MERGE=0: a free lane always starts the next batch beside a running one (no merging)
+static bool merge_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("TFHE_AMD_TIER1_MERGE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static int coalesce_window_us() {
     static const int v = [] {
         const char *e = getenv("TFHE_AMD_TIER1_WINDOW_US");
@@ -1136,7 +1148,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         // hold at most one ciphertext per CU, a second launch beside it only shares its CUs (two
         // latency-class launches of 31 run 2.15 ms each; one of 62 about 1.8), so wait for that batch
         // and take its callers' next gates too
-        if (q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= kQueueMergeLimit) {
+        if (merge_enabled() && q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= kQueueMergeLimit) {
             const auto t0 = std::chrono::steady_clock::now();
             q.arrive_cv.wait(lk, [&] { return q.in_flight == 0; });
             bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1147,9 +1159,9 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
             if (ok) {
                 const double w = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
                 q.wait_avg_us = q.wait_avg_us > 0 ? 0.8 * q.wait_avg_us + 0.2 * w : w;
-                q.window_us = std::min(1000.0, std::max(20.0, 4.0 * q.wait_avg_us + 20.0));
+                q.window_us = std::min(1000.0, std::max(kWindowFloorUs, 4.0 * q.wait_avg_us + 20.0));
             } else {
-                q.window_us = std::max(20.0, 0.75 * q.window_us);
+                q.window_us = std::max(kWindowFloorUs, 0.75 * q.window_us);
                 q.returning = 0;   // the released callers did not come back: stop expecting them
             }
             bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
