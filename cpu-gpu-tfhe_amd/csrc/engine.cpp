@@ -1150,16 +1150,28 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     int32_t *hb = h + nin * A, *db = d + nin * A;
     HostTrace tr;
     {
+        // staged and copied in in two row halves above 512 gates (each >= 1 MB, so that the copy
+        // pool takes it), the first half's copy in flight while the second is staged: of the copy
+        // in, only the second half's stays on the call's critical path
+        const int nch = B > 512 ? 2 : 1;
         std::vector<CopyJob> jobs;
-        for (int k = 0; k < nin; ++k) {
-            jobs.push_back({h + k * A, in_a[k], A * 4});
-            jobs.push_back({hb + (size_t)k * B, in_b[k], (size_t)B * 4});
-        }
         tr.lap(tr.issue);
-        HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+        for (int ch = 0; ch < nch; ++ch) {
+            const size_t r0 = (size_t)B * ch / nch, r1 = (size_t)B * (ch + 1) / nch;
+            jobs.clear();
+            for (int k = 0; k < nin; ++k) {
+                jobs.push_back({h + k * A + r0 * kn, in_a[k] + r0 * kn, (r1 - r0) * kn * 4});
+                jobs.push_back({hb + (size_t)k * B + r0, in_b[k] + r0, (r1 - r0) * 4});
+            }
+            HostCopyPool::get().copy(jobs.data(), (int)jobs.size());
+            for (int k = 0; k < nin; ++k)
+                HIPCHK(hipMemcpyAsync(d + k * A + r0 * kn, h + k * A + r0 * kn, (r1 - r0) * kn * 4,
+                                      hipMemcpyHostToDevice, c->stream));
+            if (ch == nch - 1)
+                HIPCHK(hipMemcpyAsync(db, hb, (size_t)nin * B * 4, hipMemcpyHostToDevice, c->stream));
+        }
         tr.lap(tr.stage);
     }
-    HIPCHK(hipMemcpyAsync(d, h, (size_t)nin * (A + B) * 4, hipMemcpyHostToDevice, c->stream));
     int32_t *hr = h + 3 * (A + B), *dr = d + 3 * (A + B);
     rc = tfhe_amd_gate_batch_dev(c, gate, B, dr, dr + A, d, db, d + A, db + B,
                                  mux ? d + 2 * A : nullptr, mux ? db + 2 * B : nullptr, c->stream);

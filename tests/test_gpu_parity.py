@@ -246,7 +246,8 @@ def test_mux_split_keyswitch(ctx, okey, keyset, rng):
 def test_host_batch_slices(ctx, okey, keyset, rng):
     """Host-pointer batches above one round are pipelined in slices of 1024 (one contiguous input
     copy per slice on a copy stream, the result copy behind each key switch); a 3-input MUX batch
-    of 2 100 (slices 1024 / 1024 / 52) decrypts right and matches the oracle at every slice seam."""
+    of 2 100 (slices 1024 / 1024 / 52) decrypts right and matches the oracle at every slice seam;
+    a one-round batch of 777 (copied in as two halves) in place."""
     B = 2100
     s, x, y = (rng.integers(0, 2, B) for _ in range(3))
     (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
@@ -254,6 +255,16 @@ def test_host_batch_slices(ctx, okey, keyset, rng):
     assert np.array_equal(keyset.decrypt(r_a, r_b), np.where(s == 1, x, y))
     idx = np.array([0, 1023, 1024, 2047, 2048, 2099])
     o_a, o_b = okey.gate_batch("MUX", sa[idx], sb[idx], xa[idx], xb[idx], ya[idx], yb[idx])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+    # one round, staged and copied in as two row halves (B > 512): the halves' seam and ends, and
+    # in place (the result arrays are the first input's)
+    B = 777
+    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
+    (xa, xb), (ya, yb) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    idx = np.array([0, 387, 388, 389, 776])
+    o_a, o_b = okey.gate_batch("XOR", xa[idx], xb[idx], ya[idx], yb[idx])
+    r_a, r_b = ctx.gate_host("XOR", xa, xb, ya, yb, out=(xa, xb))
+    assert np.array_equal(keyset.decrypt(r_a, r_b), x ^ y)
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
