@@ -97,6 +97,7 @@ struct __attribute__((aligned(16))) V6Ct {   // one ciphertext's LDS
     double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
+    int sync[2];                     // PS: the steps each wave has handed its partial sum over for
 };
 template <int C>
 struct __attribute__((aligned(16))) V6SharedC {
@@ -147,10 +148,13 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
-template <int WAVES, bool RREG, bool RSW = false>
+// PS (the paired kernel, two ciphertexts per workgroup): the two waves of a ciphertext meet through
+// LDS step counters instead of the workgroup barrier, so that the workgroup's two ciphertexts are
+// not held in lock-step (their LDS transposes then need not coincide on the CU).
+template <int WAVES, bool RREG, bool RSW = false, bool PS = false>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
-                                        uint32_t &bad V6_STAMPS_PARAM) {
+                                        uint32_t &bad, int &seq V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
@@ -280,7 +284,24 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     // the second MAC runs after the barrier and the partner-partial loads, so that its key
     // loads land during those waits (B = 1: 1.69 -> 1.65 ms, B = 1024: -1 %)
     V6_STAMP(3);
-    lds_barrier6();
+    if constexpr (PS) {
+        // release: this wave's partial sum (and everything before it in LDS) before its counter
+        seq += 1;
+        __hip_atomic_store(&sh.sync[w], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int spins = 0;; ++spins) {
+            const int v = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&sh.sync[1 - w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (v >= seq) break;
+            if (spins > (1 << 24)) {   // never expected; no hang: the guard's exact kernel recomputes it
+                bad = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    } else {
+        (void)seq;
+        lds_barrier6();
+    }
     V6_STAMP(4);
     // Inverse.  Every LDS read group is issued whole before the arithmetic that consumes it
     // (sched_barrier): at this register budget the scheduler otherwise sinks each ds_read to its use and
@@ -395,7 +416,7 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 // the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
 // exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
 // computes but writes nothing.
-template <int WAVES, bool RREG, int C = 1>
+template <int WAVES, bool RREG, int C = 1, bool PS = false>
 __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
                                            bool live = true) {
@@ -424,6 +445,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
         if (t.zb) xb += (uint32_t)t.sc * (uint32_t)t.zb[0];
         sh.barb = modswitch_2N(xb);
     }
+    if (tid < 2) sh.sync[tid] = 0;
     for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[t8_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
     __syncthreads();
@@ -449,6 +471,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
     uint32_t bad = 0;                    // some coefficient's round(4c) != 0 mod 4 (distance >= 1/8)
     int a_next = sh.bara[0];
     int own = w;                         // this wave's LDS buffer (the waves swap every step)
+    int seq = 0;                         // PS: partial sums handed over so far
     for (int i = 0; i < kn; ++i) {
         const int a = a_next;
         a_next = sh.bara[i + 1 < kn ? i + 1 : i];   // a step ahead: no LDS round trip at the loop head
@@ -462,7 +485,8 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG, RREG && C == 1>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG, RREG && C == 1, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
+                                                 seq V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
 #if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
@@ -524,7 +548,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g,
 // two ciphertexts per workgroup (4 waves): the dispatcher spreads a 4-wave workgroup over the
 // CU's 4 SIMDs, where two 2-wave workgroups sharing a CU land on 3 of them (2, 1, 1, 0 waves;
 // scripts/wave_placement.hip), so at B <= 2 CUs this keeps one wave per SIMD
-template <int WAVES>
+template <int WAVES, bool PS = false>
 __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Args g, int B, int total, int base,
                                                                      BrInput in0, BrInput in1, int32_t mu,
                                                                      int32_t *__restrict__ u_a,
@@ -542,7 +566,7 @@ __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Ar
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES, true, 2>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
+    br_v6_body<WAVES, true, 2, PS>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
 template <int WAVES, bool RREG>
@@ -597,7 +621,8 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo, bad = 0;
         // RREG: the throughput launches' form (the scalar-branch permutation, RSW), so that the
         // forced rotation edges of test_register_rotation_edges reach it
-        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad V6_STAMPS_ARG);
+        int seq = 0;
+        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, seq V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -718,6 +743,12 @@ static bool v6_pair(const DeviceKey &key, long n) {
 }
 // the register / ds_bpermute rotation (cmux_v6 RREG) for launches of more than one workgroup
 // per CU; TFHE_AMD_V6_RREG=0/1 forces it off/on (experiments, tests)
+// the paired kernel's waves meet per ciphertext through LDS counters instead of the workgroup
+// barrier (cmux_v6 PS); TFHE_AMD_V6P_PAIRSYNC=0/1 (experiment)
+static bool v6p_pairsync() {
+    static const char *env = getenv("TFHE_AMD_V6P_PAIRSYNC");
+    return env ? atoi(env) != 0 : false;
+}
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -752,9 +783,15 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
         const long n = total - base < chunk ? total - base : chunk;
         if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
-            trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
-            hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                               v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+            if (v6p_pairsync()) {
+                trace_kernel("k_blind_rotate_v6p(paired+reg-rotation+pair-sync)");
+                hipLaunchKernelGGL((k_blind_rotate_v6p<kV6Waves, true>), dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+            } else {
+                trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
+                hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+            }
         } else {
             trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6(reg-rotation)" : "k_blind_rotate_v6(lds-rotation)");
             if (v6_rreg(key, n))
