@@ -1114,7 +1114,10 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     q.inside += 1;
     if (q.returning > 0) q.returning -= 1;
     q.pending.push_back(&req);
-    q.arrive_cv.notify_all();   // a collecting leader may be waiting for this thread
+    // a collecting leader waits for every expected caller: wake it only when this arrival completes
+    // the set (not once per arrival: with 64 callers on a 16-CPU share those wake-ups cost as much
+    // as the batch's own host work)
+    if (q.collecting && (int)q.pending.size() >= q.inside - q.in_flight + q.returning) q.arrive_cv.notify_all();
     // a free lane and no leader collecting: the oldest pending request's thread is asked to lead
     auto appoint = [&] {
         if (!q.collecting && q.running < kQueueLanes && !q.pending.empty() && q.pending.front() != &req)
