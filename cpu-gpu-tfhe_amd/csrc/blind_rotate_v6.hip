@@ -148,9 +148,11 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
-// PS (the paired kernel, two ciphertexts per workgroup): the two waves of a ciphertext meet through
-// LDS step counters instead of the workgroup barrier, so that the workgroup's two ciphertexts are
-// not held in lock-step (their LDS transposes then need not coincide on the CU).
+// PS (the paired kernel, two ciphertexts per workgroup, the default there): the two waves of a
+// ciphertext meet through LDS step counters instead of the workgroup barrier, so that the
+// workgroup's two ciphertexts are not held in lock-step.  With one wave per SIMD nothing hides a
+// wave's LDS round trips; in lock-step the four waves of a CU issued their transposes together and
+// queued behind each other on the CU's LDS, out of step they interleave (B = 512: -12 %).
 template <int WAVES, bool RREG, bool RSW = false, bool PS = false>
 __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
@@ -744,10 +746,11 @@ static bool v6_pair(const DeviceKey &key, long n) {
 // the register / ds_bpermute rotation (cmux_v6 RREG) for launches of more than one workgroup
 // per CU; TFHE_AMD_V6_RREG=0/1 forces it off/on (experiments, tests)
 // the paired kernel's waves meet per ciphertext through LDS counters instead of the workgroup
-// barrier (cmux_v6 PS); TFHE_AMD_V6P_PAIRSYNC=0/1 (experiment)
+// barrier (cmux_v6 PS): B = 512 2.004 vs 2.277 ms, B = 384 1.995 vs 2.274 (profiles/r04j_pairsync_ab.txt);
+// TFHE_AMD_V6P_PAIRSYNC=0 restores the barrier
 static bool v6p_pairsync() {
     static const char *env = getenv("TFHE_AMD_V6P_PAIRSYNC");
-    return env ? atoi(env) != 0 : false;
+    return env ? atoi(env) != 0 : true;
 }
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");

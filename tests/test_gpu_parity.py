@@ -158,13 +158,15 @@ def test_chunk_boundaries_bit_exact(ctx, okey, keyset, rng):
 
 def test_paired_workgroups_bit_exact(ctx, okey, keyset, rng):
     """Launches of CUs < n <= 2 CUs ciphertexts (256 CUs) run two ciphertexts per workgroup
-    (k_blind_rotate_v6p): an odd count (a padding ciphertext that writes nothing), MUX halves
-    meeting inside one workgroup, and a_i = 0 steps, which the paired kernel runs as identity
-    CMuxes instead of skipping — every output against the oracle."""
+    (k_blind_rotate_v6p, whose waves meet per ciphertext through LDS step counters): an odd count
+    (a padding ciphertext that writes nothing), MUX halves meeting inside one workgroup, and
+    a_i = 0 steps, which the paired kernel runs as identity CMuxes instead of skipping — every
+    output against the oracle."""
     B = 301
     x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
     (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
     r_a, r_b = ctx.gate_host("AND", a_a, a_b, b_a, b_b)
+    assert any("v6p(paired+reg-rotation+pair-sync)" in k for k in ctx.last_kernels()), ctx.last_kernels()
     o_a, o_b = okey.gate_batch("AND", a_a, a_b, b_a, b_b)
     assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
     B = 199                                   # MUX: 398 rotations; rotations 198 | 199 share a workgroup
@@ -399,6 +401,36 @@ print("rreg ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "rreg ok" in r.stdout
+
+
+def test_paired_barrier_variant_subprocess():
+    """TFHE_AMD_V6P_PAIRSYNC=0 (read once per process) runs the paired kernel with the workgroup
+    barrier instead of the per-ciphertext LDS counters: a 301-gate batch (an odd count, so one
+    padding ciphertext) and a 199-gate MUX batch equal the oracle."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [%r, %r]
+import tfhe_amd as T, oracle_ctypes as O
+K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); o = O.OracleKey(K.bk, K.ksk)
+rng = np.random.default_rng(6)
+x, y = rng.integers(0, 2, 301), rng.integers(0, 2, 301)
+(a_a, a_b), (b_a, b_b) = K.encrypt(x, rng), K.encrypt(y, rng)
+r = c.gate_host("NAND", a_a, a_b, b_a, b_b)
+assert any("v6p(paired+reg-rotation)" in k for k in c.last_kernels()), c.last_kernels()
+w = o.gate_batch("NAND", a_a, a_b, b_a, b_b)
+assert np.array_equal(r[0], w[0]) and np.array_equal(r[1], w[1])
+s, x, y = (rng.integers(0, 2, 199) for _ in range(3))
+(sa, sb), (xa, xb), (ya, yb) = (K.encrypt(v, rng) for v in (s, x, y))
+r = c.gate_host("MUX", sa, sb, xa, xb, ya, yb); w = o.gate_batch("MUX", sa, sb, xa, xb, ya, yb)
+assert np.array_equal(r[0], w[0]) and np.array_equal(r[1], w[1])
+print("barrier ok")
+""" % (os.path.join(REPO, "cpu-gpu-tfhe_amd"), os.path.join(REPO, "tests"))
+    env = dict(os.environ, TFHE_AMD_V6P_PAIRSYNC="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "barrier ok" in r.stdout
 
 
 def test_fp64_ceiling_measurement():
