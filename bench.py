@@ -536,7 +536,7 @@ def main():
         if b == B or b <= 0:
             continue
         steps = max(3, min(args.steps, int(200 / b) + 5)) if b < 64 else max(3, args.steps // 2)
-        el, pr, ok, _, _ = timed(b, steps, 1, profile=True)
+        el, pr, ok, _, _ = timed(b, steps, 3, profile=True)   # 3 warm-up steps at the leg's own batch
         extras[str(b)] = {"value": shard.weak_scaling_value(b, world, steps, el), "ms_per_step": el / steps * 1e3,
                           "steps": steps, "kernel_ms": pr["br_ms"] / max(1, pr["br_launches"]),
                           "keyswitch_ms": pr["ks_ms"] / max(1, pr["ks_launches"]), "truth_table_ok": ok}

@@ -530,7 +530,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
 #endif
 }
 
-template <int WAVES, bool RREG, bool PS = false>
+template <int WAVES, bool RREG>
 __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g, int B, int base, BrInput in0,
                                                                 BrInput in1, int32_t mu, int32_t *__restrict__ u_a,
                                                                 int32_t *__restrict__ u_b) {
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6(V6Args g,
     t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
     t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
     t.za = nullptr; t.zb = nullptr;
-    br_v6_body<WAVES, RREG, 1, PS>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
+    br_v6_body<WAVES, RREG>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct);
 }
 
 // two ciphertexts per workgroup (4 waves): the dispatcher spreads a 4-wave workgroup over the
@@ -752,12 +752,9 @@ static bool v6p_pairsync() {
     static const char *env = getenv("TFHE_AMD_V6P_PAIRSYNC");
     return env ? atoi(env) != 0 : true;
 }
-// the one-ciphertext kernel's two waves through LDS counters too (TFHE_AMD_V6_PAIRSYNC=1, experiment:
-// there the barrier couples only the ciphertext's own two waves)
-static bool v6_pairsync() {
-    static const char *env = getenv("TFHE_AMD_V6_PAIRSYNC");
-    return env && atoi(env) != 0;
-}
+// (the one-ciphertext kernel's two waves through the same LDS counters, where the barrier couples
+// only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms,
+// profiles/r04k_v6_pairsync_ab.txt)
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -803,10 +800,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
             }
         } else {
             trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6(reg-rotation)" : "k_blind_rotate_v6(lds-rotation)");
-            if (v6_rreg(key, n) && v6_pairsync())
-                hipLaunchKernelGGL((k_blind_rotate_v6<kV6Waves, true, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                                   v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
-            else if (v6_rreg(key, n))
+            if (v6_rreg(key, n))
                 hipLaunchKernelGGL((k_blind_rotate_v6<kV6Waves, true>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
                                    v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
             else
