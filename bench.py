@@ -504,31 +504,6 @@ def main():
         "engine": T.version(),
     }
 
-    # clock under this load (rank 0 samples its own GPU; other ranks keep their GPUs busy too)
-    if not args.no_clock and fft:
-        clk = sample_clock(local, main_step)
-        torch.cuda.synchronize()
-        if clk:
-            held = FP64_PEAK_TFLOPS * clk["mhz"] / PEAK_CLOCK_MHZ
-            roof["clock"] = {"gfx_mhz": clk["mhz"], "samples": clk["samples"],
-                             "fp64_peak_at_clock": held, "frac_at_clock": roof["achieved"] / held}
-    # the fp64 rate the chip sustains under its power limit (tfhe_amd_fp64_ceiling: register-
-    # operand FMA chains on every SIMD), at the kernel's occupancy and at the best one
-    if not args.no_ceiling and fft:
-        ceil = {}
-        for wps in (2, 8):
-            tf, mhz = T.fp64_ceiling(local, wps, 2.0)
-            ceil[wps] = (tf, mhz)
-        roof["sustained"] = {
-            "tflops_at_occupancy": ceil[2][0], "mhz_at_occupancy": ceil[2][1], "waves_per_simd": 2,
-            "frac_at_occupancy": roof["achieved"] / ceil[2][0],
-            "tflops_best": ceil[8][0], "mhz_best": ceil[8][1], "frac_best": roof["achieved"] / ceil[8][0],
-            "note": "fp64 FMA chains on register operands on every SIMD for 2 s (no memory, no LDS): "
-                    "the rate the chip holds under its power limit; k_blind_rotate_v6 runs 2 waves "
-                    "per SIMD at B = 1024 (DESIGN.md 5.1)"}
-    if world > 1:
-        dist.barrier()
-
     # the metric's other batch sizes (per GPU, weak scaling like the headline)
     extras = {}
     for s in (v for v in args.extra_batches.split(",") if v.strip() and v.strip() not in ("none", "''")):
@@ -570,6 +545,33 @@ def main():
             hp[str(b)] = {"value": b / ms * 1e3, "ms_per_call": ms, "calls": len(ts), "statistic": "median",
                           "truth_table_ok": ok}
         line["host_path"] = hp
+
+    # clock under this load (rank 0 samples its own GPU; other ranks keep their GPUs busy too) and
+    # the sustained fp64 ceiling: after the timed legs, whose clocks the seconds of full-power load
+    # these two runs put on the chip would otherwise lower
+    if not args.no_clock and fft:
+        clk = sample_clock(local, main_step)
+        torch.cuda.synchronize()
+        if clk:
+            held = FP64_PEAK_TFLOPS * clk["mhz"] / PEAK_CLOCK_MHZ
+            roof["clock"] = {"gfx_mhz": clk["mhz"], "samples": clk["samples"],
+                             "fp64_peak_at_clock": held, "frac_at_clock": roof["achieved"] / held}
+    # the fp64 rate the chip sustains under its power limit (tfhe_amd_fp64_ceiling: register-
+    # operand FMA chains on every SIMD), at the kernel's occupancy and at the best one
+    if not args.no_ceiling and fft:
+        ceil = {}
+        for wps in (2, 8):
+            tf, mhz = T.fp64_ceiling(local, wps, 2.0)
+            ceil[wps] = (tf, mhz)
+        roof["sustained"] = {
+            "tflops_at_occupancy": ceil[2][0], "mhz_at_occupancy": ceil[2][1], "waves_per_simd": 2,
+            "frac_at_occupancy": roof["achieved"] / ceil[2][0],
+            "tflops_best": ceil[8][0], "mhz_best": ceil[8][1], "frac_best": roof["achieved"] / ceil[8][0],
+            "note": "fp64 FMA chains on register operands on every SIMD for 2 s (no memory, no LDS): "
+                    "the rate the chip holds under its power limit; k_blind_rotate_v6 runs 2 waves "
+                    "per SIMD at B = 1024 (DESIGN.md 5.1)"}
+    if world > 1:
+        dist.barrier()
 
     # one process driving every visible GPU through the library (tfhe_amd_multi_gate_batch_dev:
     # device-resident shards, one key replica per device, no collective) — what a C++ host such as
