@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+# (historical record of a round-4 session: it ran variants since retired — v9 / the one-wave key-prefetch build — and is kept with the profiles it produced, not for re-running)
 # GPU box, round 4: new/changed tests, the v9 A/B sweep, the Tier-1 queue rate, the host-path
 # rate and the host copy micro-benchmark (each step under its own time limit; stops on a fault)
 set -u

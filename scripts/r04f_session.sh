@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+# (historical record of a round-4 session: it ran variants since retired — v9 / the one-wave key-prefetch build — and is kept with the profiles it produced, not for re-running)
 # GPU box, round 4 session f: (1) the host copy pool + pinned readback (host path, LweSample batch,
 # Tier-1 queue with its per-phase times), (2) the paired kernel's one-wave build with a whole step
 # of key prefetch (TFHE_AMD_V6P_PF=1): parity, then an A/B at the batches it serves
