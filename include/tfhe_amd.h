@@ -201,7 +201,10 @@ int tfhe_gpu_boots_batch(int gate, int32_t *res_a, int32_t *res_b, const int32_t
                          const TFheGateBootstrappingCloudKeySet *bk);
 
 /* Convenience: the same batch over LweSample arrays (Tier-1 structs) with the device
- * context cached per cloud key. */
+ * context cached per cloud key.  Each sample's a row is gathered straight into pinned staging and
+ * each result scattered straight back (slices of 1 024 pipelined); result may be the same array as
+ * an input; current_variance is set as the reference's lweKeySwitch sets it (summed on the GPU in
+ * the reference's order).  Returns TFHE_AMD_OK or an error code (c may be NULL unless gate = MUX). */
 int tfhe_amd_boots_batch(int gate, LweSample *result, const LweSample *a, const LweSample *b,
                          const LweSample *c, int B, const TFheGateBootstrappingCloudKeySet *bk);
 
