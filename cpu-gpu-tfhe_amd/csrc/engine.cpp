@@ -1327,8 +1327,9 @@ extern "C" int tfhe_amd_keyswitch_batch_host(TfheAmdContext *c, int B, const int
 int tfhe_amd_internal_unsliced_max() { return host_slice() > 0 ? host_slice() : 1 << 30; }
 
 // The extracted samples (key-switch inputs) of this context's last gate batch of at most one
-// round (unsliced host path), halves x B rows of kN words: the Tier-1 API derives the
-// key-switched output's current_variance from their digits (tfhe_api.cpp ks_variance).
+// round (unsliced host path), halves x B rows of kN words: the Tier-1 API's per-thread-lane mode
+// (TFHE_AMD_TIER1_COALESCE=0) and raw tfhe_bootstrap_FFT derive the key-switched output's
+// current_variance from their digits (tfhe_api.cpp ks_variance).
 int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a) {
     if (!c || B <= 0 || halves < 1 || halves > 2 || (size_t)halves * B > 2 * (size_t)c->cap) return TFHE_AMD_E_ARG;
     DeviceScope dev_scope(c->device);
@@ -1336,8 +1337,7 @@ int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     const size_t bytes = sizeof(int32_t) * (size_t)halves * B * kN;
     // through the context's pinned readback buffer: a D2H straight into the caller's (pageable,
-    // often freshly allocated) array costs a fixed ~0.3 ms per call, which the Tier-1 queue's
-    // batches paid on their critical path
+    // often freshly allocated) array costs a fixed ~0.3 ms per call
     if (bytes > c->h_u_bytes) {
         if (c->h_u) (void)hipHostFree(c->h_u);
         c->h_u = nullptr;

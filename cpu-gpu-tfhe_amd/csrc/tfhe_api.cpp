@@ -994,8 +994,8 @@ static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
 // A batch of queued gates holding more than one gate kind runs as ONE mixed launch per 512 gates
 // (tfhe_amd_gate_batch_mixed_host: one blind rotation + one key switch for all kinds; run_tier1_batch
 // below takes the single-kind batches).  Inputs are staged before anything is written, so a result
-// may alias any input of its own call; each request gets its key-switch input back, from which its
-// caller sums current_variance as the single-gate path.
+// may alias any input of its own call; current_variance comes from the device
+// (tfhe_amd_internal_mixed_variance, in the reference's order of adds).
 using Tier1Clock = std::chrono::steady_clock;
 static double ms_since(Tier1Clock::time_point &t) {
     const Tier1Clock::time_point now = Tier1Clock::now();
