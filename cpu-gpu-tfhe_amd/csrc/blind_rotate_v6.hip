@@ -760,19 +760,22 @@ static bool v6_rreg(const DeviceKey &key, long n) {
     if (env) return atoi(env) != 0;
     return n > v6_cus(key);
 }
-static int v6_prio_policy(const DeviceKey &key, long wgs) {
+// (the paired kernel, one wave per SIMD, has no SIMD partner to arbitrate against: no policy,
+// B = 512 1.984-1.991 vs 2.003-2.005 ms with policy 5, profiles/r04r_prio_sweep.txt)
+static int v6_prio_policy(const DeviceKey &key, long wgs, bool paired = false) {
     static const char *env = getenv("TFHE_AMD_PRIO");
     if (env) return atoi(env);
+    if (paired) return 0;
     return wgs > 4L * v6_cus(key) ? 1 : 5;
 }
 
-static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullptr) {
+static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullptr, bool paired = false) {
     V6Args g;
     g.bk = key.bk_fft;
     g.flags = guard ? guard->flags : nullptr;
     g.stats = guard ? guard->stats : nullptr;
     g.tw = key.tw6;
-    g.prio = wgs > 0 ? v6_prio_policy(key, wgs) : 0;
+    g.prio = wgs > 0 ? v6_prio_policy(key, wgs, paired) : 0;
     static const char *sh = getenv("TFHE_AMD_PRIO_S");
     g.prio_shift = sh ? atoi(sh) : 3;
     g.cus = v6_cus(key);
@@ -792,11 +795,11 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
             if (v6p_pairsync()) {
                 trace_kernel("k_blind_rotate_v6p(paired+reg-rotation+pair-sync)");
                 hipLaunchKernelGGL((k_blind_rotate_v6p<kV6Waves, true>), dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+                                   v6_args(key, wgs, guard, true), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
             } else {
                 trace_kernel("k_blind_rotate_v6p(paired+reg-rotation)");
                 hipLaunchKernelGGL(k_blind_rotate_v6p<kV6Waves>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+                                   v6_args(key, wgs, guard, true), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
             }
         } else {
             trace_kernel(v6_rreg(key, n) ? "k_blind_rotate_v6(reg-rotation)" : "k_blind_rotate_v6(lds-rotation)");
