@@ -530,7 +530,7 @@ def main():
     if args.strong_batch > 0:
         lo, hi = shard.shard_range(args.strong_batch, rank, world)
         steps = max(3, args.steps // 2)
-        el, _, ok, _, _ = timed(hi - lo, steps, 1)
+        el, _, ok, _, _ = timed(hi - lo, steps, 3, warm_s=0.3)   # warmed up at its own batch, as the legs
         line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
                           "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
                           "steps": steps, "truth_table_ok": ok}
