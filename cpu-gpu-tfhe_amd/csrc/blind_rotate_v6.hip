@@ -753,8 +753,9 @@ static bool v6p_pairsync() {
     return env ? atoi(env) != 0 : true;
 }
 // (the one-ciphertext kernel's two waves through the same LDS counters, where the barrier couples
-// only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms,
-// profiles/r04k_v6_pairsync_ab.txt)
+// only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms, B = 1 / 64
+// / 256 1.676 / 1.713 / 1.726 vs 1.642 / 1.693 / 1.695 ms — a barrier between two waves in step is
+// cheaper than polling: profiles/r04k_v6_pairsync_ab.txt, r04w_v6_pairsync_small_ab.txt)
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
