@@ -166,7 +166,13 @@ def _check(rc, what):
 
 
 def i32(x):
-    return np.ascontiguousarray(np.asarray(x, dtype=np.int64).astype(np.int32))
+    """int32, C-contiguous view of x: the array itself when it already is one (the host batch paths
+    then read the caller's memory directly instead of a fresh copy per call — 2 copies of every
+    input, ~0.3 ms per 1 024-gate call), else a copy with the values reduced mod 2^32."""
+    a = np.asarray(x)
+    if a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]:
+        return a
+    return np.ascontiguousarray(a.astype(np.int64).astype(np.int32))
 
 
 # --------------------------------------------------------------------- files (tfhe_io.h)
