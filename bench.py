@@ -359,11 +359,41 @@ def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
     idx = np.unique(np.concatenate([np.array(seams, dtype=np.int64), rest.astype(np.int64)]))
     ok = O.OracleKey(K.bk, K.ksk, use_ntt=True)
     o_a, o_b = ok.gate_batch(gate, a_a[idx], a_b[idx], b_a[idx], b_b[idx])
-    bad = int(np.sum(np.any(g_a[idx] != o_a, axis=1) | (g_b[idx] != o_b)))
-    if world > 1:
-        bad = int(shard.max_over_ranks(float(bad), device=red_dev))
-    return {"checked_per_rank": int(len(idx)), "mismatches": bad, "vs": "exact CPU oracle (oracle/tfhe_oracle.c)",
-            "what": "outputs of the timed batch, Torus32 words (a[500], b)"}
+    local_bad = int(np.sum(np.any(g_a[idx] != o_a, axis=1) | (g_b[idx] != o_b)))
+    bad = int(shard.max_over_ranks(float(local_bad), device=red_dev)) if world > 1 else local_bad
+    return {"checked_per_rank": int(len(idx)), "mismatches": bad, "mismatches_local": local_bad,
+            "vs": "exact CPU oracle (oracle/tfhe_oracle.c)",
+            "what": "outputs of the timed batch, Torus32 words (a[500], b); mismatches = max over ranks"}
+
+
+def device_identity(torch, local):
+    """This rank's GPU as the runtime reports it: PCI domain:bus:device and UUID."""
+    p = torch.cuda.get_device_properties(local)
+    uuid = getattr(p, "uuid", None)
+    return {"device": local, "name": p.name, "cus": p.multi_processor_count,
+            "pci": "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                       getattr(p, "pci_device_id", 0)),
+            "uuid": None if uuid is None else str(uuid)}
+
+
+def rank_block(dist, torch, local, backend, rank, world, truth_ok, parity, strong_ok, ms_per_step):
+    """Gathered from every rank (all_gather_object: the only collective besides the timing max): its
+    device identity, its headline step time, truth table and oracle parity, and its strong-leg truth
+    table.  With RCCL ("nccl") every rank must sit on its own physical GPU: asserted on the PCI ids
+    and UUIDs (a gloo rehearsal may share one GPU between ranks)."""
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **device_identity(torch, local),
+            "ms_per_step": ms_per_step, "truth_table_ok": truth_ok,
+            "parity_checked": parity.get("checked_per_rank"), "parity_mismatches_local": parity.get("mismatches_local"),
+            "strong_truth_table_ok": strong_ok}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    allr.sort(key=lambda r: r["rank"])
+    pcis, uuids = [r["pci"] for r in allr], [r["uuid"] for r in allr]
+    distinct = len(set(pcis)) == world and (None in uuids or len(set(uuids)) == world)
+    if backend == "nccl":
+        assert distinct, f"RCCL world of {world} ranks but devices are not distinct: {pcis} {uuids}"
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "distinct_devices": distinct,
+            "per_rank": allr}
 
 
 def main():
@@ -409,6 +439,8 @@ def main():
         ctx.reserve(B)
         return x, y, dev, r_a, r_b, (a_a, a_b, b_a, b_b)
 
+    local_el = [0.0]   # this rank's own elapsed time of the last timed() (before the max over ranks)
+
     def timed(B, steps, warmup, profile=False, warm_s=0.0):
         """W warmup + K timed steps of batch B, barrier + synchronize on both sides, max over
         ranks; returns (elapsed_s, profile dict, truth_ok, step, batch record).  warm_s: keep
@@ -440,7 +472,8 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        el = shard.max_over_ranks(time.perf_counter() - t0, device=red_dev)
+        local_el[0] = time.perf_counter() - t0
+        el = shard.max_over_ranks(local_el[0], device=red_dev)
         prof = None
         if profile:
             prof = ctx.profile_read()
@@ -454,6 +487,7 @@ def main():
 
     B = args.batch
     elapsed, prof, truth_ok, main_step, rec = timed(B, args.steps, args.warmup, profile=True)
+    local_ms_per_step = local_el[0] / args.steps * 1e3
     parity = headline_parity(K, args.gate, rec, args.parity_samples, rank, world, red_dev)
 
     br_ms = prof["br_ms"] / max(1, prof["br_launches"])
@@ -527,33 +561,53 @@ def main():
     if extras:
         line["batches"] = extras
     # strong scaling of one global batch over the ranks (contiguous shards, shard.py)
+    strong_ok = None
     if args.strong_batch > 0:
         lo, hi = shard.shard_range(args.strong_batch, rank, world)
         steps = max(3, args.steps // 2)
-        el, _, ok, _, _ = timed(hi - lo, steps, 3, warm_s=0.3)   # warmed up at its own batch, as the legs
+        el, _, strong_ok, _, _ = timed(hi - lo, steps, 3, warm_s=0.3)   # warmed up at its own batch, as the legs
         line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
                           "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
-                          "steps": steps, "truth_table_ok": ok}
+                          "steps": steps, "truth_table_ok": strong_ok}
+
+    # every rank's identity and results (N > 1): the world the line was measured on, proven from the
+    # ranks themselves — each one's device (PCI bus id, UUID) and its own truth-table / parity checks
+    if world > 1:
+        line["ranks"] = rank_block(dist, torch, local, backend, rank, world, truth_ok, parity, strong_ok,
+                                   local_ms_per_step)
+        if line.get("strong") is not None:
+            line["strong"]["truth_table_ok_per_rank"] = [r["strong_truth_table_ok"] for r in line["ranks"]["per_rank"]]
 
     # the host-pointer API (tfhe_amd_gate_batch_host: inputs and results in host memory, staged
     # through pinned buffers, slices of 1 024 pipelined): PCIe-inclusive, never `value`
     if world == 1 and args.host_batches not in ("none", "", "''"):
-        hp = {}
+        hp, hs = {}, {}
         for s_ in args.host_batches.split(","):
             b = int(s_)
             x, y, dev, r_a, r_b, host_in = make_batch(b)
-            out = (np.zeros((b, 500), np.int32), np.zeros(b, np.int32))
-            ts = []
-            for k in range(7):
-                t0 = time.perf_counter()
-                ctx.gate_host(args.gate, *host_in, out=out)
-                if k >= 2:   # the first calls size the staging and warm the copy threads
-                    ts.append(time.perf_counter() - t0)
-            ms = float(np.median(ts)) * 1e3
-            ok = bool(np.array_equal(K.decrypt(*out), 1 - (x & y))) if args.gate == "NAND" else None
-            hp[str(b)] = {"value": b / ms * 1e3, "ms_per_call": ms, "calls": len(ts), "statistic": "median",
-                          "truth_table_ok": ok}
+            # pinned: the caller owns page-locked arrays (T.host_empty = tfhe_amd_host_alloc), the call
+            # DMAs straight from and into them; staged: ordinary (pageable) arrays, staged by the library
+            pin_in = [T.host_copy(v) for v in host_in]
+            modes = (("pinned", pin_in, (T.host_empty((b, 500)), T.host_empty(b)), hp),
+                     ("staged", host_in, (np.zeros((b, 500), np.int32), np.zeros(b, np.int32)), hs))
+            for mode, inp, out, dst in modes:
+                ts = []
+                for k in range(7):
+                    t0 = time.perf_counter()
+                    ctx.gate_host(args.gate, *inp, out=out)
+                    if k >= 2:   # the first calls size the staging and warm the copy threads
+                        ts.append(time.perf_counter() - t0)
+                ms = float(np.median(ts)) * 1e3
+                ok = bool(np.array_equal(K.decrypt(*out), 1 - (x & y))) if args.gate == "NAND" else None
+                dst[str(b)] = {"value": b / ms * 1e3, "ms_per_call": ms, "calls": len(ts), "statistic": "median",
+                               "truth_table_ok": ok, "arrays": mode,
+                               "vs_device_ms_per_step": ms / line["ms_per_step"] if b == B else None}
+        for d_ in (hp, hs):   # against the device path at the same batch (the headline or a `batches` leg)
+            for k_, e_ in d_.items():
+                dv = value if int(k_) == B else extras.get(k_, {}).get("value")
+                e_["vs_device_value"] = None if not dv else e_["value"] / dv
         line["host_path"] = hp
+        line["host_path_staged"] = hs
 
     # clock under this load (rank 0 samples its own GPU; other ranks keep their GPUs busy too) and
     # the sustained fp64 ceiling: after the timed legs, whose clocks the seconds of full-power load

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <condition_variable>
@@ -1107,8 +1108,129 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
     return rc;
 }
 
+// Caller-owned pinned buffers.  A registry of the library's own page-locked
+// allocations, [start, start + bytes): a call whose every array lies inside one of them DMAs straight
+// from and to the caller's memory.  Caching hipHostRegister of arbitrary caller arrays was ruled out
+// (a registration outlives a free + malloc that reuses the address); here the library
+// allocates and frees, so a registered range is always the memory it was registered for.
+namespace {
+class PinnedRegistry {
+public:
+    static PinnedRegistry &get() {
+        static PinnedRegistry *r = new PinnedRegistry();   // never destroyed: used from atexit paths
+        return *r;
+    }
+    void add(void *p, size_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        blocks_[(uintptr_t)p] = bytes;
+    }
+    bool remove(void *p) {
+        std::lock_guard<std::mutex> lk(mu_);
+        return blocks_.erase((uintptr_t)p) != 0;
+    }
+    bool contains(const void *p, size_t bytes) {
+        if (!p) return false;
+        const uintptr_t a = (uintptr_t)p;
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = blocks_.upper_bound(a);
+        if (it == blocks_.begin()) return false;
+        --it;
+        return a >= it->first && bytes <= it->second && a - it->first <= it->second - bytes;
+    }
+
+private:
+    std::mutex mu_;
+    std::map<uintptr_t, size_t> blocks_;
+};
+}  // namespace
+
+extern "C" void *tfhe_amd_host_alloc(size_t bytes) {
+    if (bytes == 0) bytes = 1;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    PinnedRegistry::get().add(p, bytes);
+    return p;
+}
+
+extern "C" int tfhe_amd_host_free(void *p) {
+    if (!p || !PinnedRegistry::get().remove(p)) return TFHE_AMD_E_ARG;
+    return hipHostFree(p) == hipSuccess ? TFHE_AMD_OK : TFHE_AMD_E_HIP;
+}
+
+extern "C" int tfhe_amd_host_is_pinned(const void *p, size_t bytes) {
+    return PinnedRegistry::get().contains(p, bytes) ? 1 : 0;
+}
+
+// A host batch whose arrays are all caller-owned pinned buffers: no staging.  Same device layout
+// and slicing as gate_batch_host_sliced — slice s's inputs [a_0 | a_1 (| a_2) | b_0 | b_1 (| b_2)]
+// at word R nin s0, its results [res_a | res_b] at 3 R B + R s0 — but the copies read and write
+// the caller's arrays: every slice's b words first, on the compute stream (small copies run as blit
+// kernels, which must not queue behind a blind rotation holding every CU), then per slice its `a`
+// rows by DMA on the copy stream (slice s + 1's beside slice s's blind rotation) and its results
+// back on the compute stream behind its key switch.  Nothing runs on the host but the enqueueing.
+// Slices touch disjoint rows, so results that alias inputs are still read before they are written.
+static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
+                                  const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
+    constexpr size_t R = kn + 1;
+    const int S = host_slice() > 0 ? host_slice() : B;
+    const int nsl = (B + S - 1) / S;
+    if (nsl > 1 && !c->copy_in) {
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
+        for (hipEvent_t *e : {&c->ev_in, &c->ev_out[0], &c->ev_out[1]})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    int32_t *d = c->io;
+    const size_t out0 = 3 * R * (size_t)B;
+    HostTrace tr;
+    auto drain = [&] {
+        if (c->copy_in) (void)hipStreamSynchronize(c->copy_in);
+        (void)hipStreamSynchronize(c->stream);
+    };
+    hipError_t e = hipSuccess;
+    for (int s = 0; s < nsl && e == hipSuccess; ++s) {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        int32_t *db = d + R * (size_t)nin * s0 + (size_t)nin * n * kn;
+        for (int k = 0; k < nin && e == hipSuccess; ++k)
+            e = hipMemcpyAsync(db + (size_t)k * n, in_b[k] + s0, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
+    }
+    for (int s = 0; s < nsl && e == hipSuccess; ++s) {
+        const int s0 = s * S, n = std::min(S, B - s0);
+        const size_t na = (size_t)n * kn;
+        int32_t *di = d + R * (size_t)nin * s0;
+        hipStream_t cin = nsl > 1 ? c->copy_in : c->stream;
+        for (int k = 0; k < nin && e == hipSuccess; ++k)
+            e = hipMemcpyAsync(di + k * na, in_a[k] + (size_t)s0 * kn, na * 4, hipMemcpyHostToDevice, cin);
+        if (e == hipSuccess && nsl > 1) e = hipEventRecord(c->ev_in, c->copy_in);
+        if (e == hipSuccess && nsl > 1) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
+        if (e != hipSuccess) break;
+        const int32_t *da = di, *db = di + nin * na;
+        int32_t *dout = d + out0 + R * (size_t)s0;
+        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, da, db, da + na, db + n,
+                                               nin > 2 ? da + 2 * na : nullptr, nin > 2 ? db + 2 * n : nullptr,
+                                               c->stream);
+        if (rc) {
+            drain();
+            return rc;
+        }
+        e = hipMemcpyAsync(res_a + (size_t)s0 * kn, dout, na * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(res_b + s0, dout + na, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+    }
+    tr.lap(tr.issue);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    tr.lap(tr.wait);
+    if (e != hipSuccess) {
+        drain();
+        HIPCHK(e);
+    }
+    tr.report("pinned", B);
+    return TFHE_AMD_OK;
+}
+
 // host batch: stage inputs into pinned memory, one H2D, the device batch, one D2H (sliced and
-// pipelined above one round).
+// pipelined above one round); arrays that are all caller-owned pinned buffers skip the staging.
 extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                         const int32_t *ca_a, const int32_t *ca_b, const int32_t *cb_a,
                                         const int32_t *cb_b, const int32_t *cc_a, const int32_t *cc_b) {
@@ -1128,6 +1250,15 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
     TraceScope trace(c);
     int rc = tfhe_amd_reserve(c, B);
     if (rc) return rc;
+    {
+        const int nin = mux ? 3 : 2;
+        const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
+        PinnedRegistry &pr = PinnedRegistry::get();
+        const size_t A = (size_t)B * kn * 4, Bb = (size_t)B * 4;
+        bool pinned = pr.contains(res_a, A) && pr.contains(res_b, Bb);
+        for (int k = 0; k < nin && pinned; ++k) pinned = pr.contains(in_a[k], A) && pr.contains(in_b[k], Bb);
+        if (pinned) return gate_batch_host_pinned(c, gate, B, res_a, res_b, in_a, in_b, nin);
+    }
     if (host_slice() > 0 && B > host_slice()) {
         const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
         rc = gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);

@@ -1,4 +1,4 @@
-// keyswitch.hip — lweKeySwitch as a coalesced gather-accumulate on gfx950.
+// keyswitch.hip — lweKeySwitch on gfx950: three kernels by batch size.
 //
 // Reference path replaced (gpuParallel/):
 //   lweKeySwitch                       lwe-keyswitch-functions.cu:955-987
@@ -9,10 +9,13 @@
 // kernel did 8192 dependent gathers per thread with the b-sum and the accumulator
 // round-tripped through the host.
 //
-// Device KSK layout: [i < 1024][j < 8][h-1 < 3][512] int32, a row = 500 a + b + pad (2 KB).
-// v1: one 512-thread workgroup per ciphertext, thread k owns output coefficient k
-// (k == 500 is b); every (i, j) step is one 2 KB coalesced row read.  Digits are wave-
-// uniform (same (i, j) for all lanes), so the aij == 0 skip never diverges.
+//  * k_keyswitch_v5 (the default above the small-batch threshold): the key switch as an exact
+//    int8 MFMA product — the 1024 x 8 base-4 digits as a one-hot matrix, the key as four signed
+//    byte limbs, v_mfma_i32_32x32x32_i8 tiles, limbs recombined with wrapping shifts;
+//  * k_keyswitch_small (<= 12 key switches, and circuit rows): row gathers from the KSK rows
+//    [i < 1024][j < 8][h-1 < 3][512] int32 (a row = 500 a + b + pad, 2 KB), split over chunks
+//    of key indices with wrapping atomics;
+//  * k_keyswitch_v4 (TFHE_AMD_KS5=0): lane = ciphertext, LDS-staged key column blocks.
 #include "engine.h"
 #include "modarith.h"
 

@@ -62,6 +62,10 @@ def _load():
     for f in ("tfhe_amd_gate_batch_dev",):
         getattr(L, f).argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_VP] * 8 + [_VP]
     L.tfhe_amd_gate_batch_host.argtypes = [_VP, ctypes.c_int, ctypes.c_int] + [_I32P] * 8
+    L.tfhe_amd_host_alloc.restype = _VP
+    L.tfhe_amd_host_alloc.argtypes = [ctypes.c_size_t]
+    L.tfhe_amd_host_free.argtypes = [_VP]
+    L.tfhe_amd_host_is_pinned.argtypes = [_VP, ctypes.c_size_t]
     L.tfhe_amd_gate_batch_mixed_host.argtypes = [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_int)] + [_I32P] * 8
     L.tfhe_amd_bootstrap_woks_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
     L.tfhe_amd_bootstrap_batch_dev.argtypes = [_VP, ctypes.c_int, ctypes.c_int32] + [_VP] * 4 + [_VP]
@@ -173,6 +177,45 @@ def i32(x):
     if a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]:
         return a
     return np.ascontiguousarray(a.astype(np.int64).astype(np.int32))
+
+
+class _PinnedBlock:
+    """one tfhe_amd_host_alloc buffer, freed when the last array viewing it goes"""
+
+    def __init__(self, nbytes):
+        self.ptr = lib.tfhe_amd_host_alloc(max(1, nbytes))
+        if not self.ptr:
+            raise TfheAmdError(f"tfhe_amd_host_alloc({nbytes}) failed")
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and lib is not None:
+            lib.tfhe_amd_host_free(self.ptr)
+            self.ptr = None
+
+
+def host_empty(shape, dtype=np.int32):
+    """A numpy array in caller-owned pinned host memory (tfhe_amd_host_alloc).  Host batch calls
+    whose arrays are all such arrays DMA straight from and into them, with no staging copy."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    blk = _PinnedBlock(n)
+    buf = (ctypes.c_char * max(1, n)).from_address(blk.ptr)
+    buf._owner = blk
+    return np.frombuffer(buf, dtype=dt, count=n // dt.itemsize).reshape(shape)
+
+
+def host_copy(x, dtype=np.int32):
+    """x copied into a new pinned array (host_empty)"""
+    a = np.asarray(x)
+    out = host_empty(a.shape, dtype)
+    out[...] = a
+    return out
+
+
+def is_pinned(a):
+    """whether the array's bytes lie inside one tfhe_amd_host_alloc buffer"""
+    a = np.asarray(a)
+    return bool(lib.tfhe_amd_host_is_pinned(a.ctypes.data, a.nbytes))
 
 
 # --------------------------------------------------------------------- files (tfhe_io.h)
@@ -401,7 +444,8 @@ class Context:
 
     # ---- host (numpy) batches
     def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, out=None):
-        """tfhe_amd_gate_batch_host; out = (r_a [B][500], r_b [B]) int32 arrays to reuse (else new ones)."""
+        """tfhe_amd_gate_batch_host; out = (r_a [B][500], r_b [B]) int32 arrays to reuse (else new ones).
+        With every array pinned (host_empty / host_copy) the call DMAs straight from and into them."""
         g = GATES[gate] if isinstance(gate, str) else int(gate)
         ca_a = i32(ca_a); B = ca_a.shape[0]
         if out is not None:

@@ -25,6 +25,7 @@
 #define TFHE_AMD_H
 
 #include <stdint.h>
+#include <stddef.h>
 #include "tfhe/tfhe_core.h"
 
 #ifdef __cplusplus
@@ -90,6 +91,18 @@ int tfhe_amd_gate_batch_host(TfheAmdContext *ctx, int gate, int B,
                              const int32_t *ca_a, const int32_t *ca_b,
                              const int32_t *cb_a, const int32_t *cb_b,
                              const int32_t *cc_a, const int32_t *cc_b);
+
+/* Caller-owned pinned host buffers (page-locked, portable to every device).  When every array of a
+ * tfhe_amd_gate_batch_host call lies inside buffers from tfhe_amd_host_alloc, the call skips the
+ * library's pinned staging: its inputs are copied by DMA straight from the caller's arrays and the
+ * results straight into them (the reference's per-gate cudaMemcpy pairs, boot-gates.cu:2489-2615,
+ * become one DMA per array, overlapped with the previous slice's blind rotation above one round).
+ * Only the library's own allocations are recognised, so a freed and reused address is never
+ * mistaken for pinned memory.  tfhe_amd_host_free returns TFHE_AMD_E_ARG for a pointer that is not
+ * the start of a live buffer; tfhe_amd_host_is_pinned reports whether [p, p + bytes) lies in one. */
+void *tfhe_amd_host_alloc(size_t bytes);
+int tfhe_amd_host_free(void *p);
+int tfhe_amd_host_is_pinned(const void *p, size_t bytes);
 
 /* B gates of MIXED kinds (gates[i] = TFHE_GATE_NAND .. TFHE_GATE_MUX, a host array) in one
  * blind-rotation launch and one key-switch launch (a one-level circuit: a MUX is two rows and a

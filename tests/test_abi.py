@@ -195,3 +195,24 @@ def test_gate_constants_match_reference_modswitch():
     assert lib.modSwitchToTorus32(1, 8) == T.MU == 1 << 29
     assert lib.modSwitchToTorus32(-1, 8) == -(1 << 29)
     assert lib.modSwitchToTorus32(1, 4) == 1 << 30
+
+
+def test_pinned_registry_refuses_foreign_pointers():
+    """tfhe_amd_host_free / _is_pinned only know the library's own pinned buffers: a numpy array
+    (pageable) is never reported pinned and cannot be freed; NULL is refused."""
+    a = np.zeros(1024, np.int32)
+    assert T.lib.tfhe_amd_host_is_pinned(a.ctypes.data, a.nbytes) == 0
+    assert T.lib.tfhe_amd_host_is_pinned(None, 4) == 0
+    assert T.lib.tfhe_amd_host_free(None) == -1
+    assert T.lib.tfhe_amd_host_free(a.ctypes.data) == -1
+    assert not T.is_pinned(a)
+
+
+def test_pinned_arrays_without_gpu_fail_loudly():
+    import torch
+    if torch.cuda.is_available():
+        p = T.host_empty((4, 500))
+        assert T.is_pinned(p) and T.is_pinned(p[1:]) and p.shape == (4, 500)
+        return
+    with pytest.raises(T.TfheAmdError):
+        T.host_empty((4, 500))

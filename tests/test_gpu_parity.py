@@ -270,6 +270,44 @@ def test_host_batch_slices(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
+@pytest.mark.parametrize("gate,B", [("NAND", 64), ("NAND", 1024), ("MUX", 2100), ("AND", 777)])
+def test_pinned_host_batch_equals_device_path(ctx, okey, keyset, rng, gate, B):
+    """Caller-owned pinned arrays (tfhe_amd_host_alloc via T.host_copy / host_empty): the host call
+    DMAs straight from and into them (no staging).  Every output word equals the device path's on the
+    same inputs and the staged host path's; the slice seams match the oracle; then in place (results
+    into the first input's pinned arrays); and a call with one array not pinned takes the staged path
+    with the same results."""
+    torch = _torch()
+    nin = 3 if gate == "MUX" else 2
+    bits = [rng.integers(0, 2, B) for _ in range(nin)]
+    host = [v for b in bits for v in keyset.encrypt(b, rng)]
+    pin = [T.host_copy(v) for v in host]
+    assert all(T.is_pinned(p) for p in pin) and not T.is_pinned(host[0])
+    out = (T.host_empty((B, n)), T.host_empty(B))
+    r_a, r_b = ctx.gate_host(gate, *pin, out=out)
+    dev = [torch.from_numpy(v).cuda() for v in host]
+    d_a = torch.empty((B, n), dtype=torch.int32, device="cuda")
+    d_b = torch.empty(B, dtype=torch.int32, device="cuda")
+    ctx.reserve(B)
+    ctx.gate_dev(gate, d_a, d_b, *dev)
+    ctx.sync()
+    w_a, w_b = d_a.cpu().numpy(), d_b.cpu().numpy()
+    assert np.array_equal(r_a, w_a) and np.array_equal(r_b, w_b)
+    s_a, s_b = ctx.gate_host(gate, *host)                   # staged (pageable arrays)
+    assert np.array_equal(s_a, w_a) and np.array_equal(s_b, w_b)
+    idx = np.unique(np.array([0, B // 2, B - 1] + [i for i in (1023, 1024, 2047, 2048) if i < B]))
+    o_a, o_b = okey.gate_batch(gate, *[h[idx] for h in host])
+    assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
+    # in place: the results overwrite the first input's pinned arrays
+    r2 = ctx.gate_host(gate, *pin, out=(pin[0], pin[1]))
+    assert r2[0] is pin[0] and np.array_equal(pin[0], w_a) and np.array_equal(pin[1], w_b)
+    # one input pageable: the staged path, same words
+    mixed = [T.host_copy(v) for v in host]
+    mixed[2] = host[2].copy()
+    m_a, m_b = ctx.gate_host(gate, *mixed, out=(T.host_empty((B, n)), T.host_empty(B)))
+    assert np.array_equal(m_a, w_a) and np.array_equal(m_b, w_b)
+
+
 def test_large_ragged_batch(ctx, okey, keyset, rng):
     """A batch of 12 289 gates: twelve one-round blind-rotation launches plus a ragged 13th
     of one ciphertext, one key switch over all of them; every output decrypts right and the
