@@ -437,15 +437,20 @@ extern "C" int tfhe_amd_context_create_replica(TfheAmdContext *src, int device, 
         hipMalloc(&c->gstats, sizeof(uint32_t) * 4) != hipSuccess ||
         hipMemset(c->gstats, 0, sizeof(uint32_t) * 4) != hipSuccess)
         return fail(TFHE_AMD_E_HIP);
-    std::lock_guard<std::recursive_mutex> lk(src->mu);
+    // src's lock only while its pending work (the key conversions) drains and its key is snapshot:
+    // the converted key is immutable from then on, so the peer copies below run without it and the
+    // replicas of several slots (multi.cpp builds them from one worker per slot) copy concurrently
+    DeviceKey src_key;
     {
-        DeviceScope src_scope(src->device);   // src's pending work (conversions) has finished
+        std::lock_guard<std::recursive_mutex> lk(src->mu);
+        DeviceScope src_scope(src->device);
         if (hipStreamSynchronize(src->stream) != hipSuccess) return fail(TFHE_AMD_E_HIP);
+        src_key = src->key;
     }
     DeviceKey &k = c->key;
-    k = src->key;            // scalars (CRT constants, has_bk); pointers replaced below
+    k = src_key;             // scalars (CRT constants, has_bk); pointers replaced below
     k.device = device;
-    auto sb = key_buffers(src->key);
+    auto sb = key_buffers(src_key);
     auto db = key_buffers(k);
     for (size_t i = 0; i < db.size(); ++i) *db[i].first = nullptr;
     for (size_t i = 0; i < db.size(); ++i) {

@@ -12,6 +12,7 @@ import numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cpu-gpu-tfhe_amd"))
 import tfhe_amd as T  # noqa: E402
 
+PINNED = os.environ.get("HOST_PATH_PINNED", "0") == "1"   # caller-owned pinned arrays (T.host_copy)
 K = T.SecretKeyset()
 ctx = T.Context(K.bk, K.ksk, device=0)
 rng = np.random.default_rng(5)
@@ -22,6 +23,9 @@ for B in [int(b) for b in (sys.argv[1:] or ["1", "1024", "4096"])]:
     # results into reused, already-touched arrays (a C caller's buffers): fresh numpy arrays would
     # add the first-touch page faults of B x 2 KB to every call
     out = (np.zeros((B, 500), np.int32), np.zeros(B, np.int32))
+    if PINNED:
+        a_a, a_b, b_a, b_b = (T.host_copy(v) for v in (a_a, a_b, b_a, b_b))
+        out = (T.host_empty((B, 500)), T.host_empty(B))
     for _ in range(2):
         r_a, r_b = ctx.gate_host("NAND", a_a, a_b, b_a, b_b, out=out)
     reps = 15
@@ -56,6 +60,7 @@ for B in [int(b) for b in (sys.argv[1:] or ["1", "1024", "4096"])]:
     print(json.dumps({"batch": B, "ms_per_call": dt * 1e3, "ms_min": min(ts) * 1e3, "ms_mean": float(np.mean(ts)) * 1e3,
                       "statistic": "median of %d calls" % reps, "gate_bootstraps_per_s": B / dt, "truth_table_ok": ok,
                       "device_path_ms": dd * 1e3, "device_path_sync_ms": ds * 1e3, "slice": os.environ.get("TFHE_AMD_HOST_SLICE", "1024"),
-                      "path": "host pointers (pinned staging + PCIe both ways)", "engine": T.version()}))
+                      "path": "host pointers, caller-owned pinned arrays (DMA straight from and into them)" if PINNED
+                      else "host pointers (pinned staging + PCIe both ways)", "engine": T.version()}))
 ctx.close()
 K.close()
