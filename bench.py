@@ -590,6 +590,15 @@ def main():
             pin_in = [T.host_copy(v) for v in host_in]
             modes = (("pinned", pin_in, (T.host_empty((b, 500)), T.host_empty(b)), hp),
                      ("staged", host_in, (np.zeros((b, 500), np.int32), np.zeros(b, np.int32)), hs))
+            # the same batch from HBM-resident inputs, called synchronously in this leg (same clock state)
+            sync_ts = []
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < 0.3 or len(sync_ts) < 7:   # warmed up at this load first
+                t0 = time.perf_counter()
+                ctx.gate_dev(args.gate, r_a, r_b, *dev, stream=stream)
+                torch.cuda.synchronize()
+                sync_ts.append(time.perf_counter() - t0)
+            dev_sync_ms = float(np.median(sync_ts[-5:])) * 1e3
             for mode, inp, out, dst in modes:
                 ts = []
                 for k in range(7):
@@ -601,6 +610,7 @@ def main():
                 ok = bool(np.array_equal(K.decrypt(*out), 1 - (x & y))) if args.gate == "NAND" else None
                 dst[str(b)] = {"value": b / ms * 1e3, "ms_per_call": ms, "calls": len(ts), "statistic": "median",
                                "truth_table_ok": ok, "arrays": mode,
+                               "device_sync_ms_per_call": dev_sync_ms, "vs_device_sync_call": ms / dev_sync_ms,
                                "vs_device_ms_per_step": ms / line["ms_per_step"] if b == B else None}
         for d_ in (hp, hs):   # against the device path at the same batch (the headline or a `batches` leg)
             for k_, e_ in d_.items():

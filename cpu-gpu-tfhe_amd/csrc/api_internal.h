@@ -52,6 +52,9 @@ int tfhe_amd_internal_bk_coef(const TFheGateBootstrappingCloudKeySet *bk, int32_
 int tfhe_amd_internal_tier1_batch(const TFheGateBootstrappingCloudKeySet *bk, int gate, int B, int32_t *res_a,
                                   int32_t *res_b, const int32_t *a_a, const int32_t *a_b, const int32_t *b_a,
                                   const int32_t *b_b, const int32_t *c_a, const int32_t *c_b);
+// compute units of a device (hipDeviceAttributeMultiprocessorCount, cached; 256 if unknown): the
+// Tier-1 queue merges two batches while together they hold at most one ciphertext per CU
+int tfhe_amd_internal_device_cus(int device);
 // the extracted samples of a context's last gate batch (<= one round), halves x B rows of 1024
 int tfhe_amd_internal_last_extracted(TfheAmdContext *c, int B, int halves, int32_t *u_a);
 // device copy of host bytes on a context's GPU / its release; device-side current_variance of the

@@ -297,8 +297,11 @@ __global__ __launch_bounds__(kV4Threads, 2) void k_external_product_v4(V4Args g,
     const int s = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = tid & 63;
     int32_t *accg = acc + (size_t)blockIdx.x * 2 * kN;
-    for (int j = tid; j < 2 * kN; j += kV4Threads) e_store(sh.E[j >> kLogN], j & (kN - 1), (uint32_t)accg[j]);
+    // the index comes from device memory unchecked by the host: outside [0, kn) the accumulator is
+    // left as it is (whole workgroup, uniform) rather than reading past the key
     const int i = key_index[blockIdx.x];
+    if (i < 0 || i >= kn) return;
+    for (int j = tid; j < 2 * kN; j += kV4Threads) e_store(sh.E[j >> kLogN], j & (kN - 1), (uint32_t)accg[j]);
     __syncthreads();
     cmux_v4<true>(sh, g, i, 0, s, L);
     for (int j = tid; j < 2 * kN; j += kV4Threads) accg[j] = (int32_t)sh.E[j >> kLogN][j & (kN - 1)];

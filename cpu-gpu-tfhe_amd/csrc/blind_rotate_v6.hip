@@ -793,7 +793,9 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
         const long n = total - base < chunk ? total - base : chunk;
         if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
-            if (v6p_pairsync()) {
+            // the pair sync's bounded poll hands a ciphertext whose partner never arrives to the
+            // guard (bad flag -> exact recomputation): only with guard flags to hand it to
+            if (v6p_pairsync() && guard && guard->flags) {
                 trace_kernel("k_blind_rotate_v6p(paired+reg-rotation+pair-sync)");
                 hipLaunchKernelGGL((k_blind_rotate_v6p<kV6Waves, true>), dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
                                    v6_args(key, wgs, guard, true), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);

@@ -1113,6 +1113,20 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
     return rc;
 }
 
+int tfhe_amd_internal_device_cus(int device) {
+    static std::atomic<int> cus[64];   // per device; concurrent first calls store the same value
+    const int d = device >= 0 && device < 64 ? device : 0;
+    int n = cus[d].load(std::memory_order_relaxed);
+    if (!n) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) {
+            (void)hipGetLastError();
+            n = 256;
+        }
+        cus[d].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
 // Caller-owned pinned buffers.  A registry of the library's own page-locked
 // allocations, [start, start + bytes): a call whose every array lies inside one of them DMAs straight
 // from and to the caller's memory.  Caching hipHostRegister of arbitrary caller arrays was ruled out
@@ -1169,14 +1183,24 @@ extern "C" int tfhe_amd_host_is_pinned(const void *p, size_t bytes) {
     return PinnedRegistry::get().contains(p, bytes) ? 1 : 0;
 }
 
-// A host batch whose arrays are all caller-owned pinned buffers: no staging.  Same device layout
-// and slicing as gate_batch_host_sliced — slice s's inputs [a_0 | a_1 (| a_2) | b_0 | b_1 (| b_2)]
-// at word R nin s0, its results [res_a | res_b] at 3 R B + R s0 — but the copies read and write
-// the caller's arrays: every slice's b words first, on the compute stream (small copies run as blit
-// kernels, which must not queue behind a blind rotation holding every CU), then per slice its `a`
-// rows by DMA on the copy stream (slice s + 1's beside slice s's blind rotation) and its results
-// back on the compute stream behind its key switch.  Nothing runs on the host but the enqueueing.
-// Slices touch disjoint rows, so results that alias inputs are still read before they are written.
+// A host batch whose arrays are all caller-owned pinned buffers: no staging and no input copy.
+// Page-locked host memory is mapped into every GPU's address space, so the blind rotation's gate
+// prologue (and the guard's exact recomputation) read each ciphertext's inputs straight from the
+// caller's arrays over PCIe — 4 KB per ciphertext, all workgroups at once — instead of a copy in
+// before the launch (r05c trace, B = 1 024: two 2 MB H2D DMAs of 41.7 us each plus two blit copies
+// of the b words and the gaps between them, ~120 us before the blind rotation could start).  The
+// results go the other way by DMA (the key switch writes them to device memory first: its split-K
+// form adds with atomics, which are not for PCIe-mapped memory): per slice of one round, the slice's
+// result copy runs on the copy stream behind its key switch while the next slice's blind rotation
+// runs.  TFHE_AMD_PINNED_DMA_IN=1: inputs copied in by DMA instead (A/B).  Slices touch disjoint
+// rows, so results that alias inputs are still read before they are written.
+static bool pinned_dma_in() {
+    static const bool v = [] {
+        const char *e = getenv("TFHE_AMD_PINNED_DMA_IN");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                   const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
     constexpr size_t R = kn + 1;
@@ -1187,6 +1211,7 @@ static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *r
         for (hipEvent_t *e : {&c->ev_in, &c->ev_out[0], &c->ev_out[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
+    const bool dma_in = pinned_dma_in();
     int32_t *d = c->io;
     const size_t out0 = 3 * R * (size_t)B;
     HostTrace tr;
@@ -1197,40 +1222,49 @@ static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *r
     hipError_t e = hipSuccess;
     for (int s = 0; s < nsl && e == hipSuccess; ++s) {
         const int s0 = s * S, n = std::min(S, B - s0);
-        int32_t *db = d + R * (size_t)nin * s0 + (size_t)nin * n * kn;
-        for (int k = 0; k < nin && e == hipSuccess; ++k)
-            e = hipMemcpyAsync(db + (size_t)k * n, in_b[k] + s0, (size_t)n * 4, hipMemcpyHostToDevice, c->stream);
-    }
-    for (int s = 0; s < nsl && e == hipSuccess; ++s) {
-        const int s0 = s * S, n = std::min(S, B - s0);
         const size_t na = (size_t)n * kn;
-        int32_t *di = d + R * (size_t)nin * s0;
-        hipStream_t cin = nsl > 1 ? c->copy_in : c->stream;
-        for (int k = 0; k < nin && e == hipSuccess; ++k)
-            e = hipMemcpyAsync(di + k * na, in_a[k] + (size_t)s0 * kn, na * 4, hipMemcpyHostToDevice, cin);
-        if (e == hipSuccess && nsl > 1) e = hipEventRecord(c->ev_in, c->copy_in);
-        if (e == hipSuccess && nsl > 1) e = hipStreamWaitEvent(c->stream, c->ev_in, 0);
-        if (e != hipSuccess) break;
-        const int32_t *da = di, *db = di + nin * na;
+        const int32_t *xa[3], *xb[3];
+        for (int k = 0; k < nin; ++k) {
+            xa[k] = in_a[k] + (size_t)s0 * kn;
+            xb[k] = in_b[k] + s0;
+        }
+        if (dma_in) {   // A/B: the inputs copied into the slice's device block first
+            int32_t *di = d + R * (size_t)nin * s0;
+            for (int k = 0; k < nin && e == hipSuccess; ++k) {
+                e = hipMemcpyAsync(di + k * na, xa[k], na * 4, hipMemcpyHostToDevice, c->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(di + nin * na + (size_t)k * n, xb[k], (size_t)n * 4, hipMemcpyHostToDevice,
+                                       c->stream);
+                xa[k] = di + k * na;
+                xb[k] = di + nin * na + (size_t)k * n;
+            }
+            if (e != hipSuccess) break;
+        }
         int32_t *dout = d + out0 + R * (size_t)s0;
-        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, da, db, da + na, db + n,
-                                               nin > 2 ? da + 2 * na : nullptr, nin > 2 ? db + 2 * n : nullptr,
-                                               c->stream);
+        const int rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, xa[0], xb[0], xa[1], xb[1],
+                                               nin > 2 ? xa[2] : nullptr, nin > 2 ? xb[2] : nullptr, c->stream);
         if (rc) {
             drain();
             return rc;
         }
-        e = hipMemcpyAsync(res_a + (size_t)s0 * kn, dout, na * 4, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(res_b + s0, dout + na, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+        hipStream_t cout = c->stream;
+        if (nsl > 1) {   // the result copy beside the next slice's blind rotation
+            e = hipEventRecord(c->ev_out[s & 1], c->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->copy_in, c->ev_out[s & 1], 0);
+            cout = c->copy_in;
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(res_a + (size_t)s0 * kn, dout, na * 4, hipMemcpyDeviceToHost, cout);
+        if (e == hipSuccess) e = hipMemcpyAsync(res_b + s0, dout + na, (size_t)n * 4, hipMemcpyDeviceToHost, cout);
     }
     tr.lap(tr.issue);
+    if (e == hipSuccess && nsl > 1) e = hipStreamSynchronize(c->copy_in);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     tr.lap(tr.wait);
     if (e != hipSuccess) {
         drain();
         HIPCHK(e);
     }
-    tr.report("pinned", B);
+    tr.report(dma_in ? "pinned-dma-in" : "pinned", B);
     return TFHE_AMD_OK;
 }
 

@@ -587,7 +587,6 @@ struct Tier1Req {
 // follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
 // shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [200, 1000] us.
 constexpr int kQueueLanes = 2;
-constexpr int kQueueMergeLimit = 256;   // gates two lanes' batches may hold together and still merge (MI355X CUs)
 // the straggler window never drops below this: released callers come back within ~0.1 ms, and a
 // window that times out on them splits a team into partial batches (which then queue behind each
 // other); a caller that does not come back costs one such wait, after which it is no longer expected
@@ -602,6 +601,8 @@ struct Coalescer {
     int returning = 0;    // callers released by finished batches, expected back with their next gate
     bool collecting = false;   // a leader is waiting for stragglers
     bool lane_busy[kQueueLanes] = {false, false};
+    int merge_limit = 256;     // gates two lanes' batches may hold together and still merge: one
+                               // ciphertext per CU of the key's device (set when the key registers)
     double window_us = -1.0;   // adaptive straggler window (set on first use)
     double wait_avg_us = 0.0;
     long long batches = 0, gates = 0, largest = 0, overlapped = 0;
@@ -651,6 +652,7 @@ static std::shared_ptr<KeyEntry> entry_for(const LweBootstrappingKeyFFT *bkfft, 
         fprintf(stderr, "tfhe_amd: cannot create the device context (rc=%d): no usable MI355X/HIP device\n", rc);
         die_dramatically("tfhe_amd: GPU engine unavailable");
     }
+    e->q.merge_limit = tfhe_amd_internal_device_cus(tfhe_amd_context_device(e->primary));
     g_reg[k] = e;
     return e;
 }
@@ -1151,7 +1153,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         // hold at most one ciphertext per CU, a second launch beside it only shares its CUs (two
         // latency-class launches of 31 run 2.15 ms each; one of 62 about 1.8), so wait for that batch
         // and take its callers' next gates too
-        if (merge_enabled() && q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= kQueueMergeLimit) {
+        if (merge_enabled() && q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= q.merge_limit) {
             const auto t0 = std::chrono::steady_clock::now();
             q.arrive_cv.wait(lk, [&] { return q.in_flight == 0; });
             bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -146,7 +146,8 @@ int tfhe_amd_blind_rotate_dev(TfheAmdContext *ctx, int B, int iters, int32_t *ac
                               const int32_t *bara, void *stream);
 /* tGswFFTExternMulToTLwe (tgsw_functions.h:70, tgsw-fft-operations.cu:124-264) on B accumulators:
  * acc [B][2][1024] <- BK_i (x) acc with i = key_index[b] (device arrays), exact (the NTT kernel's
- * arithmetic); the reference replaces the accumulator by the product the same way. */
+ * arithmetic); the reference replaces the accumulator by the product the same way.  An index
+ * outside [0, 500) leaves its accumulator unchanged (checked on the device). */
 int tfhe_amd_external_product_dev(TfheAmdContext *ctx, int B, const int32_t *key_index, int32_t *acc,
                                   void *stream);
 

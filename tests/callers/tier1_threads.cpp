@@ -7,6 +7,12 @@
 // samples, word for word (the engine is deterministic); each must decrypt to its truth table.
 // Then 16 short-lived std::threads each run one gate and exit: every exiting thread must give
 // its lane (stream + scratch) back, so the key's lane count returns to what it was.
+// Round 5: samples compare with current_variance bit for bit, and a mixed phase runs
+// the units interleaved (consecutive calls of a thread are different kinds, MUX among them) from 8
+// threads, so the coalescing queue's batches mix kinds and their current_variance comes from the
+// mixed launch's device-side sum (tfhe_amd_internal_mixed_variance / k_ks_variance_rows), which
+// must equal the variance of the same gate run alone.  argv[2] = "nonuniform": the key-switching
+// key's row variances are made unequal before the first gate (the device sum's general form).
 // Prints one JSON line; exit status 0 only when everything matched.
 #include <cstdio>
 #include <cstdint>
@@ -38,7 +44,8 @@ static int t_orny(int a, int b) { return (!a) | b; }
 static int t_oryn(int a, int b) { return a | (!b); }
 
 static bool same(const LweSample *x, const LweSample *y, int n) {
-    return x->b == y->b && memcmp(x->a, y->a, sizeof(Torus32) * n) == 0;
+    return x->b == y->b && memcmp(x->a, y->a, sizeof(Torus32) * n) == 0 &&
+           memcmp(&x->current_variance, &y->current_variance, sizeof(double)) == 0;
 }
 
 int main(int argc, char **argv) {
@@ -56,6 +63,11 @@ int main(int argc, char **argv) {
     TFheGateBootstrappingSecretKeySet *key = new_random_gate_bootstrapping_secret_keyset(params);
     const TFheGateBootstrappingCloudKeySet *bk = &key->cloud;
     const LweParams *lp = params->in_out_params;
+    const bool nonuniform = argc > 2 && strcmp(argv[2], "nonuniform") == 0;
+    if (nonuniform) {   // unequal row variances, before the key's device tables exist
+        LweSample *rows = bk->bkFFT->ks->ks0_raw;
+        for (int r = 0; r < 1024 * 8 * 4; r++) rows[r].current_variance *= 1.0 + ((r * 37) % 11) * 1e-3;
+    }
     const int dim = lp->n;
 
     std::vector<int> xa(n), xb(n), xc(n);
@@ -74,6 +86,7 @@ int main(int argc, char **argv) {
     LweSample *seq = new_gate_bootstrapping_ciphertext_array(total, params);
     LweSample *par = new_gate_bootstrapping_ciphertext_array(total, params);
     LweSample *ali = new_gate_bootstrapping_ciphertext_array(total, params);
+    LweSample *mix = new_gate_bootstrapping_ciphertext_array(total, params);
 
     auto run = [&](int k, LweSample *out) {
         const int g = k / n, i = k % n;
@@ -99,6 +112,13 @@ int main(int argc, char **argv) {
             bootsMUX(r, &a[i], &b[i], r, bk);
         }
     }
+    // interleaved kinds: call q runs unit (q mod units) on sample (q / units), statically dealt
+    // round-robin to 8 threads, so every batch the queue forms holds several kinds (MUX included)
+#pragma omp parallel for num_threads(8) schedule(static, 1)
+    for (int q = 0; q < total; q++) {
+        const int k = (q % units) * n + q / units;
+        run(k, &mix[k]);
+    }
     // short-lived threads: one gate each, then exit
     const int lanes_before = tfhe_amd_tier1_lane_count(bk);
     int short_errors = 0;
@@ -111,19 +131,22 @@ int main(int argc, char **argv) {
         delete_gate_bootstrapping_ciphertext_array(1, r);
     }
     const int lanes_after = tfhe_amd_tier1_lane_count(bk);
-    int par_mismatch = 0, alias_mismatch = 0, truth_errors = 0;
+    int par_mismatch = 0, alias_mismatch = 0, mixed_mismatch = 0, truth_errors = 0, zero_variance = 0;
     for (int k = 0; k < total; k++) {
         const int g = k / n, i = k % n;
         par_mismatch += !same(&seq[k], &par[k], dim);
         alias_mismatch += !same(&seq[k], &ali[k], dim);
+        mixed_mismatch += !same(&seq[k], &mix[k], dim);
+        zero_variance += !(seq[k].current_variance > 0);
         const int want = g < ng ? gates[g].truth(xa[i], xb[i]) : (xa[i] ? xb[i] : xc[i]);
         truth_errors += bootsSymDecrypt(&seq[k], key) != want;
     }
     printf("{\"units\": %d, \"per_unit\": %d, \"threads\": 8, \"par_mismatch\": %d, \"alias_mismatch\": %d, "
-           "\"truth_errors\": %d, \"seq_ms_per_gate\": %.3f, \"par_ms_per_gate\": %.3f, \"lanes_before\": %d, "
+           "\"mixed_mismatch\": %d, \"zero_variance\": %d, \"nonuniform_key\": %d, \"truth_errors\": %d, \"seq_ms_per_gate\": %.3f, \"par_ms_per_gate\": %.3f, \"lanes_before\": %d, "
            "\"lanes_after_short_threads\": %d, \"short_thread_errors\": %d}\n",
-           units, n, par_mismatch, alias_mismatch, truth_errors, 1e3 * (t1 - t0) / total, 1e3 * (t2 - t1) / total,
+           units, n, par_mismatch, alias_mismatch, mixed_mismatch, zero_variance, (int)nonuniform, truth_errors, 1e3 * (t1 - t0) / total, 1e3 * (t2 - t1) / total,
            lanes_before, lanes_after, short_errors);
+    delete_gate_bootstrapping_ciphertext_array(total, mix);
     delete_gate_bootstrapping_ciphertext_array(total, ali);
     delete_gate_bootstrapping_ciphertext_array(total, par);
     delete_gate_bootstrapping_ciphertext_array(total, seq);
@@ -132,5 +155,8 @@ int main(int argc, char **argv) {
     delete_gate_bootstrapping_ciphertext_array(n, a);
     delete_gate_bootstrapping_secret_keyset(key);
     delete_gate_bootstrapping_parameters(params);
-    return par_mismatch || alias_mismatch || truth_errors || short_errors || lanes_after != lanes_before ? 1 : 0;
+    return par_mismatch || alias_mismatch || mixed_mismatch || zero_variance || truth_errors || short_errors ||
+                   lanes_after != lanes_before
+               ? 1
+               : 0;
 }

@@ -103,6 +103,26 @@ def test_external_product_exact(keyset, okey, rng):
 
 
 @pytest.mark.gpu
+def test_external_product_dev_index_checked_on_device(ctx, okey, rng):
+    """tfhe_amd_external_product_dev takes its key indices from device memory: an index outside
+    [0, 500) leaves that accumulator unchanged (no read past the key); valid neighbours
+    in the same launch still get the exact product."""
+    import torch
+    idx = np.array([3, -1, 500, 1 << 30, 499], np.int32)
+    acc = rng.integers(-2**31, 2**31, (len(idx), 2, N), dtype=np.int64).astype(np.int32)
+    d_acc = torch.from_numpy(acc.copy()).cuda()
+    d_idx = torch.from_numpy(idx).cuda()
+    rc = L.tfhe_amd_external_product_dev(ctx.h, len(idx), ctypes.c_void_p(d_idx.data_ptr()),
+                                         ctypes.c_void_p(d_acc.data_ptr()), None)
+    assert rc == 0
+    ctx.sync()
+    got = d_acc.cpu().numpy()
+    for b, i in enumerate(idx):
+        want = okey.external_product(acc[b], int(i)) if 0 <= i < 500 else acc[b]
+        assert np.array_equal(got[b], want), (b, int(i))
+
+
+@pytest.mark.gpu
 def test_blind_rotate_fft_exact(keyset, okey, rng):
     bkp, accp, _, arr = key_parts(keyset)
     t = L.new_TLweSample(accp)

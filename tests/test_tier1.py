@@ -22,17 +22,24 @@ def test_tier1_driver_builds():
 
 
 @pytest.mark.gpu
-def test_tier1_threads_and_aliasing_gpu():
-    """Every gate + MUX: sequential vs 8 OpenMP threads vs result aliasing an input give the
-    same samples word for word, and every output decrypts to its truth table; 16 short-lived
+@pytest.mark.parametrize("keyrows", ["uniform", "nonuniform"])
+def test_tier1_threads_and_aliasing_gpu(keyrows):
+    """Every gate + MUX: sequential vs 8 OpenMP threads vs result aliasing an input vs 8 threads with
+    the kinds interleaved (the queue's batches mix kinds, MUX included) give the same samples word
+    for word and current_variance bit for bit (the mixed batches' device-side variance sum against
+    the same gate run alone), on a key with the reference's equal key-switching-key row
+    variances and on one whose rows differ; every output decrypts to its truth table; 16 short-lived
     threads running one gate each leave the key's lane count unchanged."""
     assert os.access(EXE, os.X_OK), "tests/callers/_bin/tier1_threads missing: run __graft_entry__.build()"
-    r = subprocess.run([EXE, "24"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([EXE, "24"] + (["nonuniform"] if keyrows == "nonuniform" else []),
+                       capture_output=True, text=True, timeout=300)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert lines, (r.returncode, r.stderr[-2000:])
     out = json.loads(lines[-1])
     assert r.returncode == 0, (out, r.stderr[-2000:])
     assert out["par_mismatch"] == 0 and out["alias_mismatch"] == 0 and out["truth_errors"] == 0, out
+    assert out["mixed_mismatch"] == 0 and out["zero_variance"] == 0, out
+    assert out["nonuniform_key"] == (keyrows == "nonuniform"), out
     # threads that exit give their lanes back (no stream / scratch / pinned-memory leak per thread)
     assert out["short_thread_errors"] == 0 and out["lanes_after_short_threads"] == out["lanes_before"], out
 

@@ -224,5 +224,7 @@ inline hipError_t hipStreamWaitEvent(hipStream_t st, hipEvent_t e, unsigned) {
     hip_stub::enqueue(st, [e, t] { e->wait_for(t); });
     return hipSuccess;
 }
+enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 63 };
+inline hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t, int) { *v = 256; return hipSuccess; }
 inline hipError_t hipDeviceCanAccessPeer(int *can, int, int) { *can = 1; return hipSuccess; }
 inline hipError_t hipDeviceEnablePeerAccess(int, unsigned) { return hipSuccess; }
