@@ -93,15 +93,18 @@ __device__ __forceinline__ unsigned int hwreg_xcc_id() {
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #endif
 
-struct __attribute__((aligned(16))) V6Ct {   // one ciphertext's LDS
-    double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
+template <int S>
+struct __attribute__((aligned(16))) V6CtT {   // one ciphertext's LDS
+    double2 X[2][S];                 // per-wave buffer (9 KB; v10 16.5 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
     int sync[2];                     // PS: the steps each wave has handed its partial sum over for
 };
-template <int C>
+using V6Ct = V6CtT<kXSlots>;
+using V10Ct = V6CtT<kR16Slots>;      // the radix-16 forward's transpose holds both digit polynomials
+template <int C, class CT = V6Ct>
 struct __attribute__((aligned(16))) V6SharedC {
-    V6Ct ct[C];                      // C ciphertexts per workgroup share ...
+    CT ct[C];                        // C ciphertexts per workgroup share ...
     double2 tw[kT8Words];            // ... the per-lane twiddles (compact table, fft_wave.h)
 };
 using V6Shared = V6SharedC<1>;
@@ -153,8 +156,12 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // workgroup's two ciphertexts are not held in lock-step.  With one wave per SIMD nothing hides a
 // wave's LDS round trips; in lock-step the four waves of a CU issued their transposes together and
 // queued behind each other on the CU's LDS, out of step they interleave (B = 512: -12 %).
-template <int WAVES, bool RREG, bool RSW = false, bool PS = false>
-__device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, int i, int a, int w, int &own,
+// R16 (k_blind_rotate_v10): the radix-16 forward (fft_wave.h r16_pass1_transpose / r16_pass2) in
+// place of passes A, B, C: the lane then holds spectrum slots 8 r16_lane(L) + r, so the key is read
+// at that lane, and the inverse starts with the matching C -> B transpose (store_C16 / load_B16)
+template <int WAVES, bool RREG, bool RSW = false, bool PS = false, bool R16 = false, class CT = V6Ct>
+__device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, const Tw4 &tU3,
+                                        int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
                                         uint32_t &bad, int &seq V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
@@ -166,18 +173,22 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     const double2 *bk = g.bk + (size_t)i * 8 * 512 + L;
 #define KEYC(c) ((c) ^ w)
 #else
-    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
+    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + (R16 ? r16_lane(L) : L);
 #define KEYC(c) (c)
 #endif
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
     Cx D[2][8];
+    int32_t HI[R16 ? 16 : 1], LO[R16 ? 16 : 1];   // R16: the digits as integers, exchanged across lanes first
     auto digits = [&](int r, uint32_t rot) {
         const uint32_t diff = rot - acc[r];
         const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
         const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
-        if (r < 8) {
+        if constexpr (R16) {
+            HI[r] = hi;
+            LO[r] = lo;
+        } else if (r < 8) {
             D[0][r].re = (double)hi;
             D[1][r].re = (double)lo;
         } else {
@@ -262,20 +273,34 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 #else
 #define TW7(fn) fn(shtw, L)
 #endif
-    fft_fwd_AB_t<2>(D, X, tA, TW7(tw7_fwdB), L);
-    V6_STAMP(1);
+    if constexpr (R16) {
+        // radix-16 forward (one LDS transpose for both digit polynomials); the first key slice is in
+        // flight during pass 2
+        Cx Z[16];
+        r16_pass1_transpose(HI, LO, Z, X, tA, tU3, L);
+        V6_STAMP(1);
+        load_bk(bv, bk, KEYC(1 - w));
+        __builtin_amdgcn_sched_barrier(0);
+        r16_pass2(Z, D, shtw, L);
+    } else {
+        (void)tU3;
+        fft_fwd_AB_t<2>(D, X, tA, TW7(tw7_fwdB), L);
+        V6_STAMP(1);
+    }
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC, the hand-over and the barrier.
-    const Tw4 tC = TW7(tw7_fwdC);
     Cx Y[8];
     // (issuing them at the top of the step instead, in flight for the whole forward transform,
     // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
     // (a one-wave build of the paired kernel that loads each key slice a whole step ahead, 64 more
     // VGPRs live across the step, measured slower: B = 512 2.336 vs 2.273 ms, profiles/r04f_*)
-    load_bk(bv, bk, KEYC(1 - w));
-    __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
-    fft_fwd_C<2>(D, tC);
+    if constexpr (!R16) {
+        const Tw4 tC = TW7(tw7_fwdC);
+        load_bk(bv, bk, KEYC(1 - w));
+        __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
+        fft_fwd_C<2>(D, tC);
+    }
     mac6(D, bv, Y);
     V6_STAMP(2);
     load_bk(bv, bk, KEYC(w));
@@ -332,9 +357,15 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     X = sh.X[1 - own];
     own = 1 - own;
     V6_STAMP(6);
-    store_C(X, Y, L);
-    wave_sync();
-    load_B_p(X, Y, L);
+    if constexpr (R16) {
+        store_C16(X, Y, r16_lane(L));
+        wave_sync();
+        load_B16(X, Y, L);
+    } else {
+        store_C(X, Y, L);
+        wave_sync();
+        load_B_p(X, Y, L);
+    }
     SCHED_FENCE();
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
@@ -418,8 +449,15 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
 // the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
 // exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
 // computes but writes nothing.
-template <int WAVES, bool RREG, int C = 1, bool PS = false>
-__device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
+// v10 (two waves per SIMD at B > 2 CUs) takes the scalar-branch rotation (RSW) in both its forms;
+// TFHE_AMD_V10_NORSW: the paired kernel's conditional stages (A/B)
+#ifdef TFHE_AMD_V10_NORSW
+constexpr bool kV10Rsw = false;
+#else
+constexpr bool kV10Rsw = true;
+#endif
+template <int WAVES, bool RREG, int C = 1, bool PS = false, bool R16 = false, class CT = V6Ct>
+__device__ __forceinline__ void br_v6_body(CT &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
                                            bool live = true) {
     const int tid = threadIdx.x & (kV6Threads - 1);
@@ -448,8 +486,9 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
         sh.barb = modswitch_2N(xb);
     }
     if (tid < 2) sh.sync[tid] = 0;
-    for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[t8_src(e)];
+    for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[R16 ? t10_src(e) : t8_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
+    const Tw4 tU3 = R16 ? load_tw_sgpr(g.tw + kTwR16U) : tA;
     __syncthreads();
     // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
     uint32_t acc[16];
@@ -487,8 +526,8 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG, RREG && C == 1, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
-                                                 seq V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG, RREG && (C == 1 || (R16 && kV10Rsw)), PS, R16>(sh, shtw, g, tA, tU3, i, a, w, own, L, acc, mx, hlo, hhi, bad,
+                                                      seq V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
 #if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
@@ -571,6 +610,51 @@ __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Ar
     br_v6_body<WAVES, true, 2, PS>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
+// v10: the paired kernel with the radix-16 forward (cmux_v6 R16).  Its transpose needs a 16.5 KB
+// buffer per wave, so a ciphertext takes 34 KB of LDS and the workgroup's two share one compact
+// twiddle table (80 KB): 2 workgroups, 8 waves per CU, the throughput launches' occupancy.
+template <bool PS>
+__global__ __launch_bounds__(2 * kV6Threads, kV6Waves) void k_blind_rotate_v10(V6Args g, int B, int total, int base,
+                                                                        BrInput in0, BrInput in1, int32_t mu,
+                                                                        int32_t *__restrict__ u_a,
+                                                                        int32_t *__restrict__ u_b) {
+    __shared__ V6SharedC<2, V10Ct> sh;
+    const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    int gct = base + 2 * (int)blockIdx.x + s;
+    const bool live = gct < total;
+    if (!live) gct = total - 1;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+    RowTerms6 t;
+    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+    t.za = nullptr; t.zb = nullptr;
+    br_v6_body<kV6Waves, true, 2, PS, true>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct,
+                                             live);
+}
+// one ciphertext per workgroup (45 KB of LDS: 3 workgroups per CU), for launches of at most one
+// workgroup per CU (the latency regime)
+template <bool RREG>
+__global__ __launch_bounds__(kV6Threads, kV6Waves) void k_blind_rotate_v10s(V6Args g, int B, int base, BrInput in0,
+                                                                     BrInput in1, int32_t mu,
+                                                                     int32_t *__restrict__ u_a,
+                                                                     int32_t *__restrict__ u_b) {
+    __shared__ V6SharedC<1, V10Ct> sh;
+    const int gct = base + blockIdx.x;
+    const int half = gct >= B;
+    const int idx = half ? gct - B : gct;
+    const BrInput &in = half ? in1 : in0;
+    RowTerms6 t;
+    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
+    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
+    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
+    t.za = nullptr; t.zb = nullptr;
+    br_v6_body<kV6Waves, RREG, 1, false, true>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct,
+                                                (size_t)gct);
+}
+
 template <int WAVES, bool RREG>
 __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, long base,
                                                                      const CircRow *__restrict__ rows,
@@ -624,7 +708,7 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         // RREG: the throughput launches' form (the scalar-branch permutation, RSW), so that the
         // forced rotation edges of test_register_rotation_edges reach it
         int seq = 0;
-        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, seq V6_STAMPS_ARG);
+        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, seq V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -703,6 +787,17 @@ void build_v6_twiddles(double2 *tw) {
         tw[4 + 256 + 2 * 64 + L] = cis(W[8][4 * L]);
         tw[4 + 256 + 3 * 64 + L] = cis(W[8][4 * L + 2]);
     }
+    // the radix-16 forward (v10, fft_wave.h kT10P2 order; scripts/emu_v10.py)
+    for (int j = 0; j < 4; ++j) tw[kTwR16U + j] = cis(W[3][2 * j]);
+    double2 *p2 = tw + kTwR16P2;
+    for (int m = 0; m < 16; ++m) {
+        p2[kT10P2 + m] = cis(W[4][m]);
+        p2[kT10T5 + m] = cis(W[5][2 * m]);
+        for (int q = 0; q < 2; ++q) p2[kT10T6 + 16 * q + m] = cis(W[6][4 * m + 2 * q]);
+        for (int q = 0; q < 4; ++q) p2[kT10T7 + 16 * q + m] = cis(W[7][8 * m + 2 * q]);
+    }
+    for (int q = 0; q < 4; ++q)
+        for (int t = 0; t < 32; ++t) p2[kT10T8 + 32 * q + t] = cis(W[8][16 * (t & 15) + 8 * (t >> 4) + 2 * q]);
 }
 
 hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s) {
@@ -756,6 +851,18 @@ static bool v6p_pairsync() {
 // only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms, B = 1 / 64
 // / 256 1.676 / 1.713 / 1.726 vs 1.642 / 1.693 / 1.695 ms — a barrier between two waves in step is
 // cheaper than polling: profiles/r04k_v6_pairsync_ab.txt, r04w_v6_pairsync_small_ab.txt)
+// the radix-16 forward (k_blind_rotate_v10 / v10s): TFHE_AMD_V10=1 for the throughput launches
+// (n > 2 CUs, paired), 2 for every launch (one ciphertext per workgroup at n <= CUs, paired
+// above); A/B against v6.  Returns 0 (v6), 1 (v10s) or 2 (v10, paired).
+static int v10_mode(const DeviceKey &key, long n) {
+    static const char *env = getenv("TFHE_AMD_V10");
+    const int m = env ? atoi(env) : 0;
+    const long cus = v6_cus(key);
+    if (m <= 0) return 0;
+    if (n > 2 * cus) return 2;
+    if (m < 2) return 0;
+    return n > cus ? 2 : 1;
+}
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -791,7 +898,23 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        if (v6_pair(key, n)) {
+        const int v10 = v10_mode(key, n);
+        if (v10 == 1) {
+            trace_kernel("k_blind_rotate_v10s(radix-16)");
+            hipLaunchKernelGGL((k_blind_rotate_v10s<false>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
+                               v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
+        } else if (v10 == 2) {
+            const long wgs = (n + 1) / 2;
+            if (guard && guard->flags) {
+                trace_kernel("k_blind_rotate_v10(radix-16+pair-sync)");
+                hipLaunchKernelGGL(k_blind_rotate_v10<true>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+            } else {
+                trace_kernel("k_blind_rotate_v10(radix-16)");
+                hipLaunchKernelGGL(k_blind_rotate_v10<false>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
+                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
+            }
+        } else if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
             // the pair sync's bounded poll hands a ciphertext whose partner never arrives to the
             // guard (bad flag -> exact recomputation): only with guard flags to hand it to

@@ -26,7 +26,9 @@ struct DeviceKey {
 };
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
-constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64;   // double2 entries (blind_rotate_v6.hip)
+// double2 entries (blind_rotate_v6.hip): the v6 tables, then the radix-16 forward's (v10): 4 uniform
+// pass-1 twiddles and the 256-entry per-lane pass-2 table
+constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64 + 4 + 256;
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {

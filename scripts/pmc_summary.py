@@ -4,6 +4,7 @@ kernels over the headline's timed launches only (dispatch order: W warm-up steps
 ones, each step = blind rotation + guard launch + key switch), HBM bytes per launch, and the
 blind rotation's per-wave-step instruction counts (B ciphertexts x 2 waves x 500 CMux steps).
     python scripts/pmc_summary.py <pass_dir> <engine> <batch> [steps] [warmup] [tag]
+(PMC_SUMMARY_OUT=<path> writes elsewhere, e.g. an A/B variant's summary)
 gfx950: FETCH_SIZE (KB) reports half the bytes of 16-B-per-lane streaming reads
 (MI355X_MICROARCH.md §HBM) -> doubled; WRITE_SIZE (KB) taken as is."""
 import csv
@@ -12,7 +13,8 @@ import json
 import os
 import sys
 
-KINDS = (("blind_rotate", lambda n: "k_blind_rotate_v6<" in n and "v6p" not in n and "v6_rows" not in n),
+KINDS = (("blind_rotate", lambda n: ("k_blind_rotate_v6<" in n and "v6p" not in n and "v6_rows" not in n)
+                          or "k_blind_rotate_v10<" in n),
          ("guard", lambda n: "k_blind_rotate_v4<" in n),
          ("keyswitch", lambda n: "k_keyswitch" in n))
 
@@ -69,7 +71,8 @@ def main():
     out = {"engine": engine, "batch": batch, "launch_selection": f"headline timed launches [{warm}, {warm + steps})",
            "kernels": kern, "source": tag, "passes": sources}
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    json.dump(out, open(os.path.join(repo, "profiles", "pmc_summary.json"), "w"), indent=1)
+    dst = os.environ.get("PMC_SUMMARY_OUT") or os.path.join(repo, "profiles", "pmc_summary.json")
+    json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
