@@ -380,7 +380,9 @@ def rank_block(dist, torch, local, backend, rank, world, truth_ok, parity, stron
     """Gathered from every rank (all_gather_object: the only collective besides the timing max): its
     device identity, its headline step time, truth table and oracle parity, and its strong-leg truth
     table.  With RCCL ("nccl") every rank must sit on its own physical GPU: asserted on the PCI ids
-    and UUIDs (a gloo rehearsal may share one GPU between ranks)."""
+    and UUIDs (a gloo rehearsal may share one GPU between ranks) — reported, and warned about on
+    stderr rather than raised, so that a partitioned part whose logical GPUs share a PCI function
+    cannot abort the scaling run (RCCL itself refuses two ranks on one device)."""
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **device_identity(torch, local),
             "ms_per_step": ms_per_step, "truth_table_ok": truth_ok,
             "parity_checked": parity.get("checked_per_rank"), "parity_mismatches_local": parity.get("mismatches_local"),
@@ -389,9 +391,9 @@ def rank_block(dist, torch, local, backend, rank, world, truth_ok, parity, stron
     dist.all_gather_object(allr, mine)
     allr.sort(key=lambda r: r["rank"])
     pcis, uuids = [r["pci"] for r in allr], [r["uuid"] for r in allr]
-    distinct = len(set(pcis)) == world and (None in uuids or len(set(uuids)) == world)
-    if backend == "nccl":
-        assert distinct, f"RCCL world of {world} ranks but devices are not distinct: {pcis} {uuids}"
+    distinct = len(set(pcis)) == world or (None not in uuids and len(set(uuids)) == world)
+    if backend == "nccl" and not distinct and rank == 0:
+        print(f"warning: RCCL world of {world} ranks but devices are not distinct: {pcis} {uuids}", file=sys.stderr)
     return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "distinct_devices": distinct,
             "per_rank": allr}
 

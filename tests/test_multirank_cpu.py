@@ -215,48 +215,45 @@ def test_two_rank_matmat_row_blocks():
         assert full == want
 
 
-def _ranks_worker(rank, world, port, same_device, out):
+def _ranks_worker(rank, world, port, mode, out):
     """bench.rank_block over gloo with the device identity stubbed (no GPU here): every rank's
-    record is gathered, and a world whose ranks share a device is refused under RCCL."""
+    record is gathered; devices count as distinct by PCI function or, failing that, by UUID (a
+    partitioned part's logical GPUs share a PCI function); a shared device is reported (a warning
+    under RCCL), never raised."""
     import sys
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = 0 if same_device else rank
+    dev = 0 if mode == "same" else rank
+    pci = 0x10 if mode != "distinct" else 0x10 + dev
     bench.device_identity = lambda torch, local: {"device": dev, "name": "stub", "cus": 256,
-                                                  "pci": "0000:%02x:00" % (0x10 + dev), "uuid": "GPU-%d" % dev}
+                                                  "pci": "0000:%02x:00" % pci, "uuid": "GPU-%d" % dev}
     parity = {"checked_per_rank": 128, "mismatches": 0, "mismatches_local": rank}
     blk = bench.rank_block(dist, None, rank, "gloo", rank, world, True, parity, rank == 0, 3.0 + rank)
-    refused = None
-    try:
-        bench.rank_block(dist, None, rank, "nccl", rank, world, True, parity, True, 3.0)
-        refused = False
-    except AssertionError:
-        refused = True
-    out.put((rank, blk, refused))
+    blk_nccl = bench.rank_block(dist, None, rank, "nccl", rank, world, True, parity, True, 3.0)
+    out.put((rank, blk, blk_nccl["distinct_devices"]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("same_device", [False, True])
-def test_two_rank_bench_ranks_block(same_device):
+@pytest.mark.parametrize("mode", ["distinct", "same", "partitioned"])
+def test_two_rank_bench_ranks_block(mode):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ranks_worker, args=(r, world, port, same_device, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ranks_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, blk, refused in res:
+    for rank, blk, distinct_nccl in res:
         assert blk["world_size"] == 2 and blk["backend"] == "gloo"
         assert [r["rank"] for r in blk["per_rank"]] == [0, 1]
         assert [r["parity_mismatches_local"] for r in blk["per_rank"]] == [0, 1]
         assert [r["strong_truth_table_ok"] for r in blk["per_rank"]] == [True, False]
-        assert blk["distinct_devices"] == (not same_device)
-        assert refused == same_device
+        assert blk["distinct_devices"] == (mode != "same") == distinct_nccl
