@@ -31,6 +31,10 @@
 //  * issue priority is steered per launch (set_prio_level): a rotation phased by the workgroup's
 //    rank on its CU for the one-round launches a batch is split into (by step if the split is
 //    disabled).
+//  * v10 (k_blind_rotate_v10 / v10s, opt-in via TFHE_AMD_V10): the same step with a radix-16
+//    forward transform — both digit polynomials in one LDS transpose, cross-lane swaps for the rest
+//    (fft_wave.h r16_*, scripts/emu_v10.py); Torus32-exact and measured neutral at the throughput
+//    batches, slower below, so v6 stays the default.
 #include <atomic>
 #include <cmath>
 #include <cstdlib>

@@ -1,7 +1,7 @@
 // fft_wave.h — one wave's share of the fp64 negacyclic FFT external product (v6 blind
 // rotation): complex type, butterflies, the three radix-8 register passes and their LDS
-// transposes, twiddle tables, the mod-2^32 rounding and the key MAC.  Design: DESIGN.md §3.1,
-// emulation: scripts/emu_v6.py.
+// transposes, twiddle tables, the mod-2^32 rounding and the key MAC; the radix-16 forward of the
+// opt-in v10.  Design: DESIGN.md §3.1 / §5.4b, emulations: scripts/emu_v6.py, scripts/emu_v10.py.
 #pragma once
 #include "engine.h"
 
