@@ -23,11 +23,15 @@ Rank 0 prints ONE JSON line.  Extra objects:
                  fp64 fraction at that clock.  `sustained` = the fp64 FMA rate the chip holds
                  under its power limit (tfhe_amd_fp64_ceiling: pure register FMA chains, at the
                  kernel's 2 waves per SIMD and at 8) and the kernel's fraction of each.
-  batches      : the same step at B = 1, 512 and 4096 per GPU (BASELINE metric's other batch
-                 sizes; 512 = the per-GPU shape of the strong-scaled 4096 at N = 8)
-  strong       : global batch 4096 split over the ranks (BASELINE: batch 4096 on 1..8 GPUs)
+  batches      : the same step at B = 1, 128, 256, 512 and 4096 per GPU (BASELINE metric's other
+                 batch sizes; 128 / 512 = the per-GPU shapes of the strong-scaled 1024 / 4096 at N = 8)
+  strong       : global batches 1024 and 4096, each split over the ranks (BASELINE: 1..8 GPUs)
   host_path    : (1 rank) the host-pointer API at B = 1024 and 4096: inputs and results in host
-                 memory, PCIe-inclusive, median call — for comparison, never `value`
+                 memory, PCIe-inclusive, median call — for comparison, never `value`; `host_path`
+                 = pageable arrays staged by the library, `host_path_pinned` = caller-owned
+                 page-locked arrays (tfhe_amd_host_alloc)
+  circuits     : BASELINE configs 3-5 wall time through the circuit engine (32-bit add, 16 x 16
+                 multiply x 256, 64 x 64 16-bit matrix-vector with rows sharded over the ranks)
   cpu_baseline : the optimized CPU port (oracle/cpu_fft.c: fp64 FFT external product, the
                  spqlios algorithm class, AVX2/AVX-512, OpenMP over gates; Torus32-identical to
                  the exact oracle) timed on this host's cores on a bounded sample (rank 0, N=1),
@@ -71,8 +75,12 @@ def parse():
                     help="untimed steps first: the clock and power state settle within ~10 (2: -2 %%)")
     ap.add_argument("--batch", type=int, default=1024, help="gates per GPU per step")
     ap.add_argument("--gate", default="NAND")
-    ap.add_argument("--extra-batches", default="1,512,4096", help="per-GPU batch sizes also timed ('none' = none)")
-    ap.add_argument("--strong-batch", type=int, default=4096, help="global batch split over the ranks (0 = skip)")
+    ap.add_argument("--extra-batches", default="1,128,256,512,4096",
+                    help="per-GPU batch sizes also timed ('none' = none); 128 / 512 = the per-GPU shapes of the "
+                         "global 1024 / 4096 at N = 8")
+    ap.add_argument("--strong-batch", default="1024,4096",
+                    help="global batches each split over the ranks ('0' or 'none' = skip)")
+    ap.add_argument("--no-circuits", action="store_true", help="skip the configs 3-5 circuit leg")
     ap.add_argument("--host-batches", default="1024,4096",
                     help="PCIe-inclusive host-pointer path also timed at these batches (rank 0 of a 1-rank run; 'none')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,6 +348,112 @@ def multi_only(args):
     K.close()
 
 
+def circuits_leg(T, torch, ctx, K, rank, world, dist, red_dev, rows5=64, shard5=8):
+    """BASELINE configs 3-5 through the batched circuit engine (csrc/circuit.cpp; SURVEY.md §8(d):
+    "plus wall time for configs 3-5").  Every level of a circuit is one blind-rotation launch over
+    (gates x instances) plus one key switch; inputs are encrypted and resident in HBM, the timed
+    region is the whole circuit between synchronize (+ barrier) calls, max over ranks; outputs are
+    decrypted afterwards and checked against integer arithmetic on every rank.
+      config 3: 32-bit ripple-carry add, one instance per rank (Cipher.cpp:348-392's operator+;
+                a dependency chain: replicas only at N > 1)
+      config 4: 16 x 16 multiply, 256 instances per rank (main.cu:1483-1579's multiplyLweSamples)
+      config 5: 64 x 64 16-bit matrix-vector product, rows sharded contiguously over the ranks
+                (main.cu:2342-2462, matrixUtility.cu:65-96); at N = 1 also one 8-row shard alone,
+                the per-rank work of the 8-GPU run."""
+    import matvec
+    import shard
+    barrier = (lambda: dist.barrier()) if world > 1 else (lambda: None)
+    rng = np.random.default_rng(5000 + rank)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def all_ok(ok):
+        return bool(shard.max_over_ranks(0.0 if ok else 1.0, device=red_dev) == 0.0)
+
+    def timed_runs(C, B, wa, wb, reps, warm=True):
+        if warm:   # compiles the schedule, uploads its tables, sizes the scratch
+            C.run_dev(ctx, B, wa, wb, stream)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            C.run_dev(ctx, B, wa, wb, stream)
+            torch.cuda.synchronize()
+            barrier()
+            ts.append(time.perf_counter() - t0)
+        return shard.max_over_ranks(float(np.median(ts)), device=red_dev)
+
+    def upload(C, wires_bits, B):
+        n_w = C.info()["wires"]
+        wa = torch.zeros((n_w, B, 500), dtype=torch.int32, device="cuda")
+        wb = torch.zeros((n_w, B), dtype=torch.int32, device="cuda")
+        for w, plane in wires_bits.items():
+            ea, eb = K.encrypt(plane, rng)
+            wa[w] = torch.from_numpy(ea).cuda()
+            wb[w] = torch.from_numpy(eb).cuda()
+        return wa, wb
+
+    def binop(name, build, nbits, B, reps, ref, what):
+        C = T.Circuit()
+        a, b = C.inputs(nbits), C.inputs(nbits)
+        outs = build(C, a, b)
+        info = C.info()
+        x, y = rng.integers(0, 2**nbits, B), rng.integers(0, 2**nbits, B)
+        bits = dict(zip(a, T.bits_of(x, nbits)))
+        bits.update(zip(b, T.bits_of(y, nbits)))
+        wa, wb = upload(C, bits, B)
+        t = timed_runs(C, B, wa, wb, reps)
+        ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+        ok = all_ok(np.array_equal(T.int_of([K.decrypt(ha[w], hb[w]) for w in outs]), ref(x, y)))
+        C.close()
+        return {"what": what, "instances_per_rank": B, "seconds": t, "bootstraps_per_instance": info["bootstraps"],
+                "depth": info["depth"], "bootstraps_per_s": info["bootstraps"] * B * world / t,
+                "statistic": f"median of {reps} runs, max over ranks", "correct": ok}
+
+    out = {}
+    out["config3_add32"] = binop("add32", lambda C, a, b: (lambda s: s[0] + [s[1]])(C.add(a, b)), 32, 1, 5,
+                                 lambda x, y: x + y, "32-bit ripple-carry add, one instance per rank")
+    out["config4_mul16_b256"] = binop("mul16", lambda C, a, b: C.mul(a, b), 16, 256, 2, lambda x, y: x * y,
+                                      "16 x 16 -> 32-bit multiply (Dadda tree), 256 instances per rank")
+    # config 5: the same matrix and vector on every rank, this rank's rows
+    data = np.random.default_rng(2024)
+    A = data.integers(0, 2**16, (rows5, 64))
+    xv = data.integers(0, 2**16, 64)
+    C, a_w, x_w, y_w = matvec.build(T, 64, 16)
+    info = C.info()
+
+    def rows_run(lo, hi, warm):
+        B = hi - lo
+        wa, wb = upload(C, matvec.instance_inputs(T, a_w, x_w, A[lo:hi], xv, 16), B)
+        t = timed_runs(C, B, wa, wb, 1, warm=warm)
+        ha, hb = wa.cpu().numpy(), wb.cpu().numpy()
+        ok = np.array_equal(T.int_of([K.decrypt(ha[w], hb[w]) for w in y_w]), A[lo:hi] @ xv)
+        return t, ok
+
+    c5 = {"matrix": f"{rows5} x 64, 16-bit entries, 64-entry vector; {len(y_w)}-bit outputs",
+          "bootstraps_per_row": info["bootstraps"], "depth": info["depth"]}
+    if world == 1:
+        # one 8-row shard first (warms the schedule's tables), then all rows, the 64-row call
+        # growing the extracted-sample scratch once (one hipMalloc)
+        ts, ok_s = rows_run(0, shard5, True)
+        t, ok = rows_run(0, rows5, False)
+        c5.update({"rows_per_rank": rows5, "seconds": t, "bootstraps_per_s": info["bootstraps"] * rows5 / t,
+                   "correct": bool(ok and ok_s),
+                   "shard_of_8": {"rows": shard5, "seconds": ts, "bootstraps_per_s": info["bootstraps"] * shard5 / ts,
+                                  "what": "one rank's share of the 8-GPU run, on this GPU"}})
+    else:
+        lo, hi = matvec.shard_rows(rows5, rank, world)
+        rows_run(lo, min(hi, lo + 1), True)                 # schedule tables + warm-up, one row
+        t, ok = rows_run(lo, hi, False)
+        c5.update({"rows_per_rank": hi - lo, "seconds": t, "bootstraps_per_s": info["bootstraps"] * rows5 / t,
+                   "correct": all_ok(ok), "scaling": "strong (rows sharded over the ranks, no collective)"})
+    C.close()
+    out["config5_matvec64"] = c5
+    out["note"] = ("circuit engine: one blind-rotation launch + one key switch per bootstrap level over all "
+                   "gates x instances (DESIGN.md §9); seconds exclude encryption / decryption")
+    return out
+
+
 def headline_parity(K, gate, rec, nsamp, rank, world, red_dev):
     """Torus32 parity of the timed batch itself: `nsamp` of its outputs (launch seams, rounds and
     a seeded random sample) against the exact CPU oracle (tests/oracle_ctypes.py, test-only
@@ -562,23 +676,30 @@ def main():
                           "keyswitch_ms": pr["ks_ms"] / max(1, pr["ks_launches"]), "truth_table_ok": ok}
     if extras:
         line["batches"] = extras
-    # strong scaling of one global batch over the ranks (contiguous shards, shard.py)
-    strong_ok = None
-    if args.strong_batch > 0:
-        lo, hi = shard.shard_range(args.strong_batch, rank, world)
+    # strong scaling of each global batch over the ranks (contiguous shards, shard.py): the metric's
+    # own 1024 (128 per GPU at N = 8) and 4096 (512 per GPU)
+    strong_ok = {}
+    strong = {}
+    for s_ in args.strong_batch.split(","):
+        if not s_.strip() or s_.strip() in ("0", "none", "''"):
+            continue
+        gb = int(s_)
+        lo, hi = shard.shard_range(gb, rank, world)
         steps = max(3, args.steps // 2)
-        el, _, strong_ok, _, _ = timed(hi - lo, steps, 3, warm_s=0.3)   # warmed up at its own batch, as the legs
-        line["strong"] = {"global_batch": args.strong_batch, "per_rank_batch": hi - lo,
-                          "value": args.strong_batch * steps / el, "ms_per_step": el / steps * 1e3,
-                          "steps": steps, "truth_table_ok": strong_ok}
+        el, _, ok_, _, _ = timed(hi - lo, steps, 3, warm_s=0.3)   # warmed up at its own batch, as the legs
+        strong_ok[str(gb)] = ok_
+        strong[str(gb)] = {"global_batch": gb, "per_rank_batch": hi - lo, "value": gb * steps / el,
+                           "ms_per_step": el / steps * 1e3, "steps": steps, "truth_table_ok": ok_}
+    if strong:
+        line["strong"] = strong
 
     # every rank's identity and results (N > 1): the world the line was measured on, proven from the
     # ranks themselves — each one's device (PCI bus id, UUID) and its own truth-table / parity checks
     if world > 1:
         line["ranks"] = rank_block(dist, torch, local, backend, rank, world, truth_ok, parity, strong_ok,
                                    local_ms_per_step)
-        if line.get("strong") is not None:
-            line["strong"]["truth_table_ok_per_rank"] = [r["strong_truth_table_ok"] for r in line["ranks"]["per_rank"]]
+        for k_, e_ in line.get("strong", {}).items():
+            e_["truth_table_ok_per_rank"] = [r["strong_truth_table_ok"].get(k_) for r in line["ranks"]["per_rank"]]
 
     # the host-pointer API (tfhe_amd_gate_batch_host: inputs and results in host memory, staged
     # through pinned buffers, slices of 1 024 pipelined): PCIe-inclusive, never `value`
@@ -621,8 +742,14 @@ def main():
             for k_, e_ in d_.items():
                 dv = value if int(k_) == B else extras.get(k_, {}).get("value")
                 e_["vs_device_value"] = None if not dv else e_["value"] / dv
-        line["host_path"] = hp
-        line["host_path_staged"] = hs
+        # `host_path` is the staged path (ordinary pageable arrays), as it was through round 4;
+        # `host_path_pinned` the caller-owned page-locked arrays (round 5)
+        line["host_path"] = hs
+        line["host_path_pinned"] = hp
+
+    # BASELINE configs 3-5 (circuits), every rank: config 5's rows sharded over the ranks
+    if not args.no_circuits:
+        line["circuits"] = circuits_leg(T, torch, ctx, K, rank, world, dist, red_dev)
 
     # clock under this load (rank 0 samples its own GPU; other ranks keep their GPUs busy too) and
     # the sustained fp64 ceiling: after the timed legs, whose clocks the seconds of full-power load

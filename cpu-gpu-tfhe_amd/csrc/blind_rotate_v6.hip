@@ -31,10 +31,9 @@
 //  * issue priority is steered per launch (set_prio_level): a rotation phased by the workgroup's
 //    rank on its CU for the one-round launches a batch is split into (by step if the split is
 //    disabled).
-//  * v10 (k_blind_rotate_v10 / v10s, opt-in via TFHE_AMD_V10): the same step with a radix-16
-//    forward transform — both digit polynomials in one LDS transpose, cross-lane swaps for the rest
-//    (fft_wave.h r16_*, scripts/emu_v10.py); Torus32-exact and measured neutral at the throughput
-//    batches, slower below, so v6 stays the default.
+//  * round 5's radix-16 generation (v10 / v10s: one LDS transpose per forward transform pair,
+//    cross-lane swaps for the rest) was exact and measured neutral at the throughput batches and
+//    slower below; it was removed in round 6 (profiles/r05i_*, r05k_*).
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -90,25 +89,18 @@ __device__ __forceinline__ unsigned int hwreg_xcc_id() {
 #define V6_STAMPS_ARG
 #endif
 
-// issue-order fence for the LDS read groups of the inverse (TFHE_AMD_V6_NOFENCE: compiler order)
-#ifdef TFHE_AMD_V6_NOFENCE
-#define SCHED_FENCE() do {} while (0)
-#else
+// issue-order fence for the LDS read groups of the inverse
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
 
-template <int S>
-struct __attribute__((aligned(16))) V6CtT {   // one ciphertext's LDS
-    double2 X[2][S];                 // per-wave buffer (9 KB; v10 16.5 KB): accumulator extension, FFT transposes, partial sums
+struct __attribute__((aligned(16))) V6Ct {   // one ciphertext's LDS
+    double2 X[2][kXSlots];           // per-wave buffer (9 KB): accumulator extension, FFT transposes, partial sums
     short bara[512];                 // rotation amounts < 2N (16 bit: 8 workgroups fit a CU)
     int barb;
     int sync[2];                     // PS: the steps each wave has handed its partial sum over for
 };
-using V6Ct = V6CtT<kXSlots>;
-using V10Ct = V6CtT<kR16Slots>;      // the radix-16 forward's transpose holds both digit polynomials
-template <int C, class CT = V6Ct>
+template <int C>
 struct __attribute__((aligned(16))) V6SharedC {
-    CT ct[C];                        // C ciphertexts per workgroup share ...
+    V6Ct ct[C];                      // C ciphertexts per workgroup share ...
     double2 tw[kT8Words];            // ... the per-lane twiddles (compact table, fft_wave.h)
 };
 using V6Shared = V6SharedC<1>;
@@ -120,7 +112,7 @@ struct V6Args {
     uint32_t *stats;     // [1]: the largest distance (high word) seen
     const double2 *tw;   // build_v6_twiddles' table; copied to LDS in compact form (fft_wave.h)
     int prio;            // issue-priority policy, see set_prio_level
-    int prio_shift;      // policies 2, 5: steps per level = 2^prio_shift
+    int prio_shift;      // policy 5: steps per level = 2^prio_shift
     int cus;             // compute units (workgroup b shares its CU with b +- cus, b +- 2 cus, ...)
 };
 
@@ -131,10 +123,10 @@ struct V6Args {
 // b +- 3 CUs (dispatch order; ranks 0/1 and 2/3 share SIMD pairs).  Policy 5 (one round of
 // workgroups, the default): every 8 steps each workgroup moves one level up (mod 4) from a start
 // level 2 x rank, so SIMD partners always sit two levels apart and trade first place every 16
-// steps (B = 1024: 3.56 ms with no policy -> 3.21).  Policy 2: the same rotation from a hashed
-// start level (3.36).  Policy 1 (more workgroups than fit at once): priority 3 - i / 128 by
-// step, so workgroups dispatched later, still early in their 500 steps, go first (B = 4096 in
-// one launch: 15.4 -> 13.7 ms).  Policy 0: hardware default.  TFHE_AMD_PRIO overrides.
+// steps (B = 1024: 3.56 ms with no policy -> 3.21; the same rotation from a hashed start level:
+// 3.36).  Policy 1 (more workgroups than fit at once): priority 3 - i / 128 by step, so
+// workgroups dispatched later, still early in their 500 steps, go first (B = 4096 in one launch:
+// 15.4 -> 13.7 ms).  Policy 0: hardware default (the paired kernel).
 __device__ __forceinline__ void set_prio_level(unsigned lvl) {
     switch (lvl & 3) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
@@ -145,13 +137,6 @@ __device__ __forceinline__ void set_prio_level(unsigned lvl) {
 }
 
 
-#ifdef TFHE_AMD_DIAG_NOTW
-__device__ __forceinline__ Tw4 diag_tw(int L) {
-    const double x = 0.70710678118654752 + 1e-9 * L;
-    return Tw4{Cx{x, -x}, Cx{-x, x}, Cx{x, x}, Cx{-x, -x}};
-}
-#endif
-
 // one CMux step, wave w: acc_w += [(X^a - 1) ACC] (x) BK_i, output polynomial w.  The
 // accumulator lives in registers; the wave's LDS buffer holds, in turn, its periodic extension
 // (rotation reads), the FFT transposes and the partial sum handed to the other wave.
@@ -160,39 +145,24 @@ __device__ __forceinline__ Tw4 diag_tw(int L) {
 // workgroup's two ciphertexts are not held in lock-step.  With one wave per SIMD nothing hides a
 // wave's LDS round trips; in lock-step the four waves of a CU issued their transposes together and
 // queued behind each other on the CU's LDS, out of step they interleave (B = 512: -12 %).
-// R16 (k_blind_rotate_v10): the radix-16 forward (fft_wave.h r16_pass1_transpose / r16_pass2) in
-// place of passes A, B, C: the lane then holds spectrum slots 8 r16_lane(L) + r, so the key is read
-// at that lane, and the inverse starts with the matching C -> B transpose (store_C16 / load_B16)
-template <int WAVES, bool RREG, bool RSW = false, bool PS = false, bool R16 = false, class CT = V6Ct>
-__device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA, const Tw4 &tU3,
+template <int WAVES, bool RREG, bool RSW = false, bool PS = false>
+__device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6Args &g, const Tw4 &tA,
                                         int i, int a, int w, int &own,
                                         int L, uint32_t (&acc)[16], double &mx, uint32_t &hlo, uint32_t &hhi,
                                         uint32_t &bad, int &seq V6_STAMPS_PARAM) {
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
-#ifdef TFHE_AMD_DIAG_SHAREBK
-    // timing diagnostic (wrong results): both waves read wave 0's key rows in wave 0's order, so
-    // the second reader of each line hits the CU's L1 (what sharing the key slice would save)
-    const double2 *bk = g.bk + (size_t)i * 8 * 512 + L;
-#define KEYC(c) ((c) ^ w)
-#else
-    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + (R16 ? r16_lane(L) : L);
-#define KEYC(c) (c)
-#endif
+    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
     Cx D[2][8];
-    int32_t HI[R16 ? 16 : 1], LO[R16 ? 16 : 1];   // R16: the digits as integers, exchanged across lanes first
     auto digits = [&](int r, uint32_t rot) {
         const uint32_t diff = rot - acc[r];
         const int32_t hi = (int32_t)(diff + (kDecompOffset + 0x80000000u)) >> 22;
         const int32_t lo = __builtin_amdgcn_sbfe((int32_t)(diff + (kDecompOffset + 0x200000u)), 12, 10);
-        if constexpr (R16) {
-            HI[r] = hi;
-            LO[r] = lo;
-        } else if (r < 8) {
+        if (r < 8) {
             D[0][r].re = (double)hi;
             D[1][r].re = (double)lo;
         } else {
@@ -259,9 +229,7 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
 #pragma unroll
         for (int r = 0; r < 16; ++r) digits(r, lo ? (r ? V[r - 1] : 0u - V[15]) : V[r]);
     } else {
-#ifndef TFHE_AMD_DIAG_NOEXT   // timing diagnostic (wrong results): no accumulator-extension stores
         write_ext(E, acc, L);
-#endif
         wave_sync();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -272,25 +240,8 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
     }
     wave_sync();
     V6_STAMP(0);
-#ifdef TFHE_AMD_DIAG_NOTW   // timing diagnostic (wrong results): twiddles from registers, no LDS loads
-#define TW7(fn) diag_tw(L)
-#else
-#define TW7(fn) fn(shtw, L)
-#endif
-    if constexpr (R16) {
-        // radix-16 forward (one LDS transpose for both digit polynomials); the first key slice is in
-        // flight during pass 2
-        Cx Z[16];
-        r16_pass1_transpose(HI, LO, Z, X, tA, tU3, L);
-        V6_STAMP(1);
-        load_bk(bv, bk, KEYC(1 - w));
-        __builtin_amdgcn_sched_barrier(0);
-        r16_pass2(Z, D, shtw, L);
-    } else {
-        (void)tU3;
-        fft_fwd_AB_t<2>(D, X, tA, TW7(tw7_fwdB), L);
-        V6_STAMP(1);
-    }
+    fft_fwd_AB_t<2>(D, X, tA, tw7_fwdB(shtw, L), L);
+    V6_STAMP(1);
     // MAC with rows 2w + p of BK_i ([p][c][r][L], slot 8 L + r): output 1 - w first, handed
     // to the other wave through this wave's buffer, then output w.  The first key slice is in
     // flight during pass C, the second during the first MAC, the hand-over and the barrier.
@@ -299,19 +250,17 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
     // measured no faster: B = 1 1.69 -> 1.75 ms, B = 1024 / 4096 unchanged)
     // (a one-wave build of the paired kernel that loads each key slice a whole step ahead, 64 more
     // VGPRs live across the step, measured slower: B = 512 2.336 vs 2.273 ms, profiles/r04f_*)
-    if constexpr (!R16) {
-        const Tw4 tC = TW7(tw7_fwdC);
-        load_bk(bv, bk, KEYC(1 - w));
+    {
+        const Tw4 tC = tw7_fwdC(shtw, L);
+        load_bk(bv, bk, 1 - w);
         __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
         fft_fwd_C<2>(D, tC);
     }
     mac6(D, bv, Y);
     V6_STAMP(2);
-    load_bk(bv, bk, KEYC(w));
+    load_bk(bv, bk, w);
     __builtin_amdgcn_sched_barrier(0);
-#ifndef TFHE_AMD_DIAG_NOHAND   // timing diagnostic (wrong results): no partial-sum hand-off
     store_C(X, Y, L);
-#endif
     // the second MAC runs after the barrier and the partner-partial loads, so that its key
     // loads land during those waits (B = 1: 1.69 -> 1.65 ms, B = 1024: -1 %)
     V6_STAMP(3);
@@ -339,12 +288,7 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
     // waits lgkmcnt(0) per pair, or per post-twist twiddle, i.e. one LDS round trip each.
     {
         Cx o[8];
-#ifdef TFHE_AMD_DIAG_NOHAND
-#pragma unroll
-        for (int r = 0; r < 8; ++r) o[r] = Y[r];
-#else
         load_C(sh.X[1 - own], o, L);
-#endif
         SCHED_FENCE();
         // the partner's partial sum seeds the second MAC (16 fp64 fewer per wave-step: B = 1 / 256
         // / 512 / 1 024 / 4 096 -0.9 / -1.2 / -0.9 / -0.8 / -0.6 %, profiles/r03_seed_mac2_ab.txt,
@@ -352,7 +296,7 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
         mac6_seeded(D, bv, o, Y);
     }
     pass_dit_C(Y);
-    const Tw4 tB = TW7(tw7_invB);
+    const Tw4 tB = tw7_invB(shtw, L);
     V6_STAMP(5);
     // Buffer hand-over instead of a second barrier: the wave goes on in the partner's buffer,
     // which the partner has finished with (it wrote its partial sum there before the barrier and
@@ -361,15 +305,9 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
     X = sh.X[1 - own];
     own = 1 - own;
     V6_STAMP(6);
-    if constexpr (R16) {
-        store_C16(X, Y, r16_lane(L));
-        wave_sync();
-        load_B16(X, Y, L);
-    } else {
-        store_C(X, Y, L);
-        wave_sync();
-        load_B_p(X, Y, L);
-    }
+    store_C(X, Y, L);
+    wave_sync();
+    load_B_p(X, Y, L);
     SCHED_FENCE();
     pass_dit(Y, tB.w0, tB.w1, tB.w2a, tB.w2b);
     {
@@ -378,19 +316,13 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
         // inputs through its first twiddle, stored as a zeta^-L — and the register factor its
         // outputs, from constants: 11 complex products and one twiddle load instead of 8 and 8
         // (B = 1024: the 8 post-twist loads alone cost 1.3 %)
-        const Tw4 tI = TW7(tw7_invA);
-#ifdef TFHE_AMD_DIAG_NOTW
-        const Cx sg = diag_tw(L).w0;
-#else
+        const Tw4 tI = tw7_invA(shtw, L);
         const Cx sg = ld(shtw + kT8Sig + L);
-#endif
-#ifndef TFHE_AMD_DIAG_NOTRAB   // timing diagnostic (wrong results): no A <-> B transposes
         wave_sync();
         store_B_ab(X, Y, L);
         wave_sync();
         load_A(X, Y, L);
         SCHED_FENCE();
-#endif
 #pragma unroll
         for (int r = 0; r < 8; r += 2) Y[r] = cmul(Y[r], sg);
         pass_dit(Y, tI.w0, tI.w1, tI.w2a, tI.w2b);
@@ -409,32 +341,6 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
     V6_STAMP(7);
     // acc_w += rint(result): coefficient L + 64 r (re) and L + 64 (r + 8) (im); mx tracks the
     // rounding distance for the exactness guard
-#ifdef TFHE_AMD_V6_GUARD_HALF
-    (void)bad;
-    // A/B experiment: measure the real parts on even steps and the imaginary parts on odd ones
-    // (every coefficient every other step; half the guard's VALU)
-    if (i & 1) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            acc[r] += (uint32_t)__double_as_longlong(Y[r].re + 0x1.8p52);
-            acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
-            acc[r + 8] += (uint32_t)__double_as_longlong(Y[r].im + 0x1.8p52);
-        }
-    }
-#elif defined(TFHE_AMD_V6_DISTGUARD)
-    // A/B: round 2's form — the distance |c - rint(c)| of every coefficient (3 fp64 + a max)
-    (void)bad;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        acc[r] += torus_of_chk(Y[r].re, mx, hlo, hhi);
-        acc[r + 8] += torus_of_chk(Y[r].im, mx, hlo, hhi);
-    }
-#else
     // the 1/8 rule on every coefficient through the quarter-ulp shifter (bad, fft_wave.h
     // torus_of_qchk: B = 1 024 / 4 096 -0.9 / -1.1 %, profiles/r03_qguard_ab.txt); the distance
     // itself on one coefficient per lane and step, for the statistic (tfhe_amd_guard_stats)
@@ -444,7 +350,6 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
         acc[r] += torus_of_qchk(Y[r].re, bad, hlo, hhi);
         acc[r + 8] += torus_of_qchk(Y[r].im, bad, hlo, hhi);
     }
-#endif
     wave_sync();
     V6_STAMP(8);
 }
@@ -453,15 +358,8 @@ __device__ __forceinline__ void cmux_v6(CT &sh, const double2 *shtw, const V6Arg
 // the workgroup's barriers lock-step both, so neither skips a_i = 0 steps (the identity CMux is
 // exact: zero digits, zero transforms, zero products).  live = false: a padding ciphertext that
 // computes but writes nothing.
-// v10 (two waves per SIMD at B > 2 CUs) takes the scalar-branch rotation (RSW) in both its forms;
-// TFHE_AMD_V10_NORSW: the paired kernel's conditional stages (A/B)
-#ifdef TFHE_AMD_V10_NORSW
-constexpr bool kV10Rsw = false;
-#else
-constexpr bool kV10Rsw = true;
-#endif
-template <int WAVES, bool RREG, int C = 1, bool PS = false, bool R16 = false, class CT = V6Ct>
-__device__ __forceinline__ void br_v6_body(CT &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
+template <int WAVES, bool RREG, int C = 1, bool PS = false>
+__device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args &g, const RowTerms6 &t, int32_t mu,
                                            int32_t *__restrict__ ua, int32_t *__restrict__ ub, size_t slot,
                                            bool live = true) {
     const int tid = threadIdx.x & (kV6Threads - 1);
@@ -490,9 +388,8 @@ __device__ __forceinline__ void br_v6_body(CT &sh, double2 *shtw, const V6Args &
         sh.barb = modswitch_2N(xb);
     }
     if (tid < 2) sh.sync[tid] = 0;
-    for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[R16 ? t10_src(e) : t8_src(e)];
+    for (int e = threadIdx.x; e < kT8Words; e += C * kV6Threads) shtw[e] = g.tw[t8_src(e)];
     const Tw4 tA = load_tw_sgpr(g.tw);
-    const Tw4 tU3 = R16 ? load_tw_sgpr(g.tw + kTwR16U) : tA;
     __syncthreads();
     // ACC = (0, X^{2N - barb} (mu, ..., mu)) (:1427-1431)
     uint32_t acc[16];
@@ -508,11 +405,7 @@ __device__ __forceinline__ void br_v6_body(CT &sh, double2 *shtw, const V6Args &
 #endif
     const int prio = g.prio;
     double mx = 0.0;                     // largest rounding distance of this lane (guard)
-#if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
-    uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo;   // range of the rounding shifter's high word (guard)
-#else
     uint32_t hlo = kQShiftHiLo, hhi = kQShiftHiLo;   // range of the rounding shifter's high word (guard)
-#endif
     uint32_t bad = 0;                    // some coefficient's round(4c) != 0 mod 4 (distance >= 1/8)
     int a_next = sh.bara[0];
     int own = w;                         // this wave's LDS buffer (the waves swap every step)
@@ -522,23 +415,16 @@ __device__ __forceinline__ void br_v6_body(CT &sh, double2 *shtw, const V6Args &
         a_next = sh.bara[i + 1 < kn ? i + 1 : i];   // a step ahead: no LDS round trip at the loop head
         if (prio == 1) {
             if ((i & 127) == 0) set_prio_level(3 - (i >> 7));
-        } else if (prio == 2) {
-            if ((i & ((1 << g.prio_shift) - 1)) == 0)
-                set_prio_level(((unsigned)blockIdx.x * 2654435761u >> 30) + ((unsigned)i >> g.prio_shift));
         } else if (prio == 5) {   // rank on the CU (dispatch order) sets the phase
             if ((i & ((1 << g.prio_shift) - 1)) == 0)
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-        cmux_v6<WAVES, RREG, RREG && (C == 1 || (R16 && kV10Rsw)), PS, R16>(sh, shtw, g, tA, tU3, i, a, w, own, L, acc, mx, hlo, hhi, bad,
-                                                      seq V6_STAMPS_ARG);
+        cmux_v6<WAVES, RREG, RREG && C == 1, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
+                                                 seq V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
-#if defined(TFHE_AMD_V6_DISTGUARD) || defined(TFHE_AMD_V6_GUARD_HALF)
-        if (hlo < kShiftHiLo || hhi >= kShiftHiEnd) mx = 0.5;   // |product| >= 2^51: not rounded exactly
-#else
         if (bad || hlo < kQShiftHiLo || hhi >= kQShiftHiEnd) mx = 0.5;   // a distance >= 1/8, or |c| >= 2^49
-#endif
         const uint32_t h = wave_max_hi(mx);
         if (L == 0) {
             g.flags[2 * slot + w] = h;
@@ -614,51 +500,6 @@ __global__ __launch_bounds__(2 * kV6Threads, WAVES) void k_blind_rotate_v6p(V6Ar
     br_v6_body<WAVES, true, 2, PS>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct, live);
 }
 
-// v10: the paired kernel with the radix-16 forward (cmux_v6 R16).  Its transpose needs a 16.5 KB
-// buffer per wave, so a ciphertext takes 34 KB of LDS and the workgroup's two share one compact
-// twiddle table (80 KB): 2 workgroups, 8 waves per CU, the throughput launches' occupancy.
-template <bool PS>
-__global__ __launch_bounds__(2 * kV6Threads, kV6Waves) void k_blind_rotate_v10(V6Args g, int B, int total, int base,
-                                                                        BrInput in0, BrInput in1, int32_t mu,
-                                                                        int32_t *__restrict__ u_a,
-                                                                        int32_t *__restrict__ u_b) {
-    __shared__ V6SharedC<2, V10Ct> sh;
-    const int s = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
-    int gct = base + 2 * (int)blockIdx.x + s;
-    const bool live = gct < total;
-    if (!live) gct = total - 1;
-    const int half = gct >= B;
-    const int idx = half ? gct - B : gct;
-    const BrInput &in = half ? in1 : in0;
-    RowTerms6 t;
-    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
-    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
-    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
-    t.za = nullptr; t.zb = nullptr;
-    br_v6_body<kV6Waves, true, 2, PS, true>(sh.ct[s], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct, (size_t)gct,
-                                             live);
-}
-// one ciphertext per workgroup (45 KB of LDS: 3 workgroups per CU), for launches of at most one
-// workgroup per CU (the latency regime)
-template <bool RREG>
-__global__ __launch_bounds__(kV6Threads, kV6Waves) void k_blind_rotate_v10s(V6Args g, int B, int base, BrInput in0,
-                                                                     BrInput in1, int32_t mu,
-                                                                     int32_t *__restrict__ u_a,
-                                                                     int32_t *__restrict__ u_b) {
-    __shared__ V6SharedC<1, V10Ct> sh;
-    const int gct = base + blockIdx.x;
-    const int half = gct >= B;
-    const int idx = half ? gct - B : gct;
-    const BrInput &in = half ? in1 : in0;
-    RowTerms6 t;
-    t.c = in.c; t.sa = in.sa; t.sb = in.sb; t.sc = 0;
-    t.xa = in.x_a + (size_t)idx * kn; t.xb = in.x_b + idx;
-    t.ya = in.sb ? in.y_a + (size_t)idx * kn : nullptr; t.yb = in.sb ? in.y_b + idx : nullptr;
-    t.za = nullptr; t.zb = nullptr;
-    br_v6_body<kV6Waves, RREG, 1, false, true>(sh.ct[0], sh.tw, g, t, mu, u_a + (size_t)gct * kN, u_b + gct,
-                                                (size_t)gct);
-}
-
 template <int WAVES, bool RREG>
 __global__ __launch_bounds__(kV6Threads, WAVES) void k_blind_rotate_v6_rows(V6Args g, int B, long base,
                                                                      const CircRow *__restrict__ rows,
@@ -708,11 +549,11 @@ __global__ __launch_bounds__(kV6Threads, 2) void k_blind_rotate_v6_debug(V6Args 
         V6Stamps stamps;
 #endif
         double mx = 0.0;
-        uint32_t hlo = kShiftHiLo, hhi = kShiftHiLo, bad = 0;
+        uint32_t hlo = kQShiftHiLo, hhi = kQShiftHiLo, bad = 0;
         // RREG: the throughput launches' form (the scalar-branch permutation, RSW), so that the
         // forced rotation edges of test_register_rotation_edges reach it
         int seq = 0;
-        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, seq V6_STAMPS_ARG);
+        cmux_v6<2, RREG, RREG>(sh.ct[0], sh.tw, g, tA, i, a, w, own, L, ac, mx, hlo, hhi, bad, seq V6_STAMPS_ARG);
     }
     __syncthreads();
 #pragma unroll
@@ -791,17 +632,6 @@ void build_v6_twiddles(double2 *tw) {
         tw[4 + 256 + 2 * 64 + L] = cis(W[8][4 * L]);
         tw[4 + 256 + 3 * 64 + L] = cis(W[8][4 * L + 2]);
     }
-    // the radix-16 forward (v10, fft_wave.h kT10P2 order; scripts/emu_v10.py)
-    for (int j = 0; j < 4; ++j) tw[kTwR16U + j] = cis(W[3][2 * j]);
-    double2 *p2 = tw + kTwR16P2;
-    for (int m = 0; m < 16; ++m) {
-        p2[kT10P2 + m] = cis(W[4][m]);
-        p2[kT10T5 + m] = cis(W[5][2 * m]);
-        for (int q = 0; q < 2; ++q) p2[kT10T6 + 16 * q + m] = cis(W[6][4 * m + 2 * q]);
-        for (int q = 0; q < 4; ++q) p2[kT10T7 + 16 * q + m] = cis(W[7][8 * m + 2 * q]);
-    }
-    for (int q = 0; q < 4; ++q)
-        for (int t = 0; t < 32; ++t) p2[kT10T8 + 32 * q + t] = cis(W[8][16 * (t & 15) + 8 * (t >> 4) + 2 * q]);
 }
 
 hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const double2 *d_tw, hipStream_t s) {
@@ -813,32 +643,24 @@ hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const doub
 // workgroups is split into launches of one round each (4 x CUs ciphertexts), each balanced by
 // the rank-phased rotation (policy 5): B = 4096 11.8-12.4 ms, against 13.4 with the hashed
 // rotation and >= 13.5 for one launch with the by-step policy.
-// TFHE_AMD_CHUNK=0 disables the split, TFHE_AMD_PRIO forces a policy (experiments).
 static int v6_cus(const DeviceKey &key) {
     static std::atomic<int> cus[64];   // per device; concurrent first calls store the same value
-    const int d = key.device >= 0 && key.device < 64 ? key.device : 0;
-    int n = cus[d].load(std::memory_order_relaxed);
+    const bool cached = key.device >= 0 && key.device < 64;
+    int n = cached ? cus[key.device].load(std::memory_order_relaxed) : 0;
     if (!n) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, key.device) != hipSuccess || n <= 0) n = 256;
-        cus[d].store(n, std::memory_order_relaxed);
+        if (cached) cus[key.device].store(n, std::memory_order_relaxed);
     }
     return n;
 }
-static long v6_chunk(const DeviceKey &key) {
-    static const char *env = getenv("TFHE_AMD_CHUNK");
-    const long c = env ? atol(env) : 4L * v6_cus(key);
-    return c > 0 ? c : (1L << 40);
-}
+static long v6_chunk(const DeviceKey &key) { return 4L * v6_cus(key); }
 // Two ciphertexts per workgroup (k_blind_rotate_v6p) for a launch of n ciphertexts when
 // CUs < n <= 2 CUs: then at most one 4-wave workgroup per CU, one wave per SIMD, where 2-wave
 // workgroups would pair up on some CUs over 3 SIMDs (B = 512: 2.36 -> 2.30 ms).  At n <= CUs
 // one 2-wave workgroup per CU is faster (B = 256: 1.74 vs 2.29 ms: 2 waves on a CU run each step
 // faster than 4 — LDS and the key path are shared per CU), and above 2 CUs the 2-wave
 // workgroups fill every SIMD (B = 768: 2.62 vs 3.18 ms, 1024: 3.12 vs 3.26).
-// TFHE_AMD_V6_PAIR=0/1 forces it off/on (experiments).
 static bool v6_pair(const DeviceKey &key, long n) {
-    static const char *env = getenv("TFHE_AMD_V6_PAIR");
-    if (env) return atoi(env) != 0;
     const long cus = v6_cus(key);
     return n > cus && n <= 2 * cus;
 }
@@ -855,18 +677,6 @@ static bool v6p_pairsync() {
 // only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms, B = 1 / 64
 // / 256 1.676 / 1.713 / 1.726 vs 1.642 / 1.693 / 1.695 ms — a barrier between two waves in step is
 // cheaper than polling: profiles/r04k_v6_pairsync_ab.txt, r04w_v6_pairsync_small_ab.txt)
-// the radix-16 forward (k_blind_rotate_v10 / v10s): TFHE_AMD_V10=1 for the throughput launches
-// (n > 2 CUs, paired), 2 for every launch (one ciphertext per workgroup at n <= CUs, paired
-// above); A/B against v6.  Returns 0 (v6), 1 (v10s) or 2 (v10, paired).
-static int v10_mode(const DeviceKey &key, long n) {
-    static const char *env = getenv("TFHE_AMD_V10");
-    const int m = env ? atoi(env) : 0;
-    const long cus = v6_cus(key);
-    if (m <= 0) return 0;
-    if (n > 2 * cus) return 2;
-    if (m < 2) return 0;
-    return n > cus ? 2 : 1;
-}
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -875,8 +685,6 @@ static bool v6_rreg(const DeviceKey &key, long n) {
 // (the paired kernel, one wave per SIMD, has no SIMD partner to arbitrate against: no policy,
 // B = 512 1.984-1.991 vs 2.003-2.005 ms with policy 5, profiles/r04r_prio_sweep.txt)
 static int v6_prio_policy(const DeviceKey &key, long wgs, bool paired = false) {
-    static const char *env = getenv("TFHE_AMD_PRIO");
-    if (env) return atoi(env);
     if (paired) return 0;
     return wgs > 4L * v6_cus(key) ? 1 : 5;
 }
@@ -888,8 +696,7 @@ static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullp
     g.stats = guard ? guard->stats : nullptr;
     g.tw = key.tw6;
     g.prio = wgs > 0 ? v6_prio_policy(key, wgs, paired) : 0;
-    static const char *sh = getenv("TFHE_AMD_PRIO_S");
-    g.prio_shift = sh ? atoi(sh) : 3;
+    g.prio_shift = 3;
     g.cus = v6_cus(key);
     return g;
 }
@@ -902,23 +709,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        const int v10 = v10_mode(key, n);
-        if (v10 == 1) {
-            trace_kernel("k_blind_rotate_v10s(radix-16)");
-            hipLaunchKernelGGL((k_blind_rotate_v10s<false>), dim3((unsigned)n), dim3(kV6Threads), 0, s,
-                               v6_args(key, n, guard), B, (int)base, in[0], in1, mu, u_a, u_b);
-        } else if (v10 == 2) {
-            const long wgs = (n + 1) / 2;
-            if (guard && guard->flags) {
-                trace_kernel("k_blind_rotate_v10(radix-16+pair-sync)");
-                hipLaunchKernelGGL(k_blind_rotate_v10<true>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
-            } else {
-                trace_kernel("k_blind_rotate_v10(radix-16)");
-                hipLaunchKernelGGL(k_blind_rotate_v10<false>, dim3((unsigned)wgs), dim3(2 * kV6Threads), 0, s,
-                                   v6_args(key, wgs, guard), B, (int)total, (int)base, in[0], in1, mu, u_a, u_b);
-            }
-        } else if (v6_pair(key, n)) {
+        if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
             // the pair sync's bounded poll hands a ciphertext whose partner never arrives to the
             // guard (bad flag -> exact recomputation): only with guard flags to hand it to

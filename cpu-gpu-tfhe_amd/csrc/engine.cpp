@@ -100,22 +100,16 @@ static std::atomic<int> g_br_version{-1};
 // round 4 (their measurements: DESIGN.md, profiles/README.md).
 static bool br_available(int v) { return v == 0 || v == 4 || v == 6; }
 
-int br_version() {
-    int v = g_br_version.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char *e = getenv("TFHE_AMD_BR");
-        v = e ? atoi(e) : 0;
-        if (!br_available(v)) v = 0;
-        g_br_version.store(v, std::memory_order_relaxed);
-    }
-    return v;
+int br_version() {   // 0 (v6, guarded) until tfhe_amd_select_kernel picks another
+    const int v = g_br_version.load(std::memory_order_relaxed);
+    return v < 0 ? 0 : v;
 }
 
 // high word of the rounding distance at which the exact kernel recomputes a ciphertext: 1/8
 // (0x3FC00000) by default — 1.6x the largest distance real keys show (0.06-0.08), so that an
 // error can only escape by reaching 7/8 at a coefficient while every other rounding of the
-// ciphertext's 500 steps stays below 1/8; tfhe_amd_set_guard_threshold changes
-// it (tests force the fallback with 0; values >= 1/2 can never trigger, the distance being <= 1/2)
+// ciphertext's 500 steps stays below 1/8; tfhe_amd_set_guard_threshold lowers
+// it (tests force the fallback with 0) and refuses anything above 1/8
 static std::atomic<uint32_t> g_guard_hi{0x3FC00000u};
 uint32_t guard_threshold_hi() { return g_guard_hi.load(std::memory_order_relaxed); }
 
@@ -600,16 +594,10 @@ static bool gate_spec(int gate, int32_t *c, int32_t *sa, int32_t *sb) {
 
 static const int32_t kMu = 1 << 29;   // modSwitchToTorus32(1, 8)
 
-// TFHE_AMD_GUARD=0 turns the guard off (A/B timing only: no flags, no exact-kernel launch)
-static bool guard_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("TFHE_AMD_GUARD");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// the exactness guard is always on: there is no switch that turns it off (tfhe_amd_set_guard_threshold
+// can only make it stricter)
 static Guard ctx_guard(TfheAmdContext *c) {
-    return c->gflags && c->gstats && guard_enabled() ? Guard{c->gflags, c->gstats} : Guard{};
+    return c->gflags && c->gstats ? Guard{c->gflags, c->gstats} : Guard{};
 }
 
 extern "C" int tfhe_amd_gate_batch_dev(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
@@ -844,8 +832,7 @@ private:
         std::condition_variable done;
     };
     HostCopyPool() {
-        const char *e = getenv("TFHE_AMD_COPY_THREADS");
-        helpers_ = std::max(0, std::min(16, e ? atoi(e) : 3));
+        helpers_ = 3;
         for (int i = 0; i < helpers_; ++i) std::thread([this] { loop(); }).detach();
     }
     static void work(Job &j) {
@@ -909,13 +896,9 @@ struct HostTrace {
     }
 };
 
-static int host_slice() {   // TFHE_AMD_HOST_SLICE overrides (0: one unsliced batch)
-    static const int v = [] {
-        const char *e = getenv("TFHE_AMD_HOST_SLICE");
-        return e ? atoi(e) : 1024;
-    }();
-    return v;
-}
+// host-pointer batches above one slice are pipelined slice by slice (one unsliced batch, every
+// copy in first and every copy out last, measured slower: profiles/r04o_*)
+static int host_slice() { return 1024; }
 
 static int gate_batch_host_sliced(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                   const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
@@ -1037,7 +1020,7 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
     constexpr size_t R = kn + 1;
     int32_t *h = c->h_io, *d = c->io;
     const size_t out0 = 3 * R * (size_t)B;
-    const int S = host_slice() > 0 ? host_slice() : B;
+    const int S = host_slice();
     const int nsl = (B + S - 1) / S;
     const int halves = mux ? 2 : 1;
     std::vector<CopyJob> jobs;
@@ -1115,14 +1098,14 @@ int tfhe_amd_internal_gate_batch_rows(TfheAmdContext *c, int gate, int B, const 
 
 int tfhe_amd_internal_device_cus(int device) {
     static std::atomic<int> cus[64];   // per device; concurrent first calls store the same value
-    const int d = device >= 0 && device < 64 ? device : 0;
-    int n = cus[d].load(std::memory_order_relaxed);
+    const bool cached = device >= 0 && device < 64;   // an out-of-range index is queried, never cached
+    int n = cached ? cus[device].load(std::memory_order_relaxed) : 0;
     if (!n) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) {
             (void)hipGetLastError();
             n = 256;
         }
-        cus[d].store(n, std::memory_order_relaxed);
+        if (cached) cus[device].store(n, std::memory_order_relaxed);
     }
     return n;
 }
@@ -1166,8 +1149,16 @@ private:
 extern "C" void *tfhe_amd_host_alloc(size_t bytes) {
     if (bytes == 0) bytes = 1;
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess || !p) {
+    // mapped into every device's address space at the same address: the pinned path's kernels read
+    // the caller's inputs through these pointers (zero-copy over PCIe), so that is checked, not assumed
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess || !p) {
         (void)hipGetLastError();
+        return nullptr;
+    }
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p) {
+        (void)hipGetLastError();
+        (void)hipHostFree(p);
         return nullptr;
     }
     PinnedRegistry::get().add(p, bytes);
@@ -1192,26 +1183,19 @@ extern "C" int tfhe_amd_host_is_pinned(const void *p, size_t bytes) {
 // results go the other way by DMA (the key switch writes them to device memory first: its split-K
 // form adds with atomics, which are not for PCIe-mapped memory): per slice of one round, the slice's
 // result copy runs on the copy stream behind its key switch while the next slice's blind rotation
-// runs.  TFHE_AMD_PINNED_DMA_IN=1: inputs copied in by DMA instead (A/B).  Slices touch disjoint
-// rows, so results that alias inputs are still read before they are written.
-static bool pinned_dma_in() {
-    static const bool v = [] {
-        const char *e = getenv("TFHE_AMD_PINNED_DMA_IN");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
+// runs.  (Copying the inputs in by DMA first measured slower: 1.064x against 1.043x the device
+// call at B = 1 024, profiles/r05d_*.)  Slices touch disjoint rows, so results that alias inputs are
+// still read before they are written.
 static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *res_a, int32_t *res_b,
                                   const int32_t *const in_a[3], const int32_t *const in_b[3], int nin) {
     constexpr size_t R = kn + 1;
-    const int S = host_slice() > 0 ? host_slice() : B;
+    const int S = host_slice();
     const int nsl = (B + S - 1) / S;
     if (nsl > 1 && !c->copy_in) {
         HIPCHK(hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking));
         for (hipEvent_t *e : {&c->ev_in, &c->ev_out[0], &c->ev_out[1]})
             HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    const bool dma_in = pinned_dma_in();
     int32_t *d = c->io;
     const size_t out0 = 3 * R * (size_t)B;
     HostTrace tr;
@@ -1227,18 +1211,6 @@ static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *r
         for (int k = 0; k < nin; ++k) {
             xa[k] = in_a[k] + (size_t)s0 * kn;
             xb[k] = in_b[k] + s0;
-        }
-        if (dma_in) {   // A/B: the inputs copied into the slice's device block first
-            int32_t *di = d + R * (size_t)nin * s0;
-            for (int k = 0; k < nin && e == hipSuccess; ++k) {
-                e = hipMemcpyAsync(di + k * na, xa[k], na * 4, hipMemcpyHostToDevice, c->stream);
-                if (e == hipSuccess)
-                    e = hipMemcpyAsync(di + nin * na + (size_t)k * n, xb[k], (size_t)n * 4, hipMemcpyHostToDevice,
-                                       c->stream);
-                xa[k] = di + k * na;
-                xb[k] = di + nin * na + (size_t)k * n;
-            }
-            if (e != hipSuccess) break;
         }
         int32_t *dout = d + out0 + R * (size_t)s0;
         const int rc = tfhe_amd_gate_batch_dev(c, gate, n, dout, dout + na, xa[0], xb[0], xa[1], xb[1],
@@ -1264,7 +1236,7 @@ static int gate_batch_host_pinned(TfheAmdContext *c, int gate, int B, int32_t *r
         drain();
         HIPCHK(e);
     }
-    tr.report(dma_in ? "pinned-dma-in" : "pinned", B);
+    tr.report("pinned", B);
     return TFHE_AMD_OK;
 }
 
@@ -1298,7 +1270,7 @@ extern "C" int tfhe_amd_gate_batch_host(TfheAmdContext *c, int gate, int B, int3
         for (int k = 0; k < nin && pinned; ++k) pinned = pr.contains(in_a[k], A) && pr.contains(in_b[k], Bb);
         if (pinned) return gate_batch_host_pinned(c, gate, B, res_a, res_b, in_a, in_b, nin);
     }
-    if (host_slice() > 0 && B > host_slice()) {
+    if (B > host_slice()) {
         const int32_t *in_a[3] = {ca_a, cb_a, cc_a}, *in_b[3] = {ca_b, cb_b, cc_b};
         rc = gate_batch_host_sliced(c, gate, B, res_a, res_b, in_a, in_b, mux ? 3 : 2);
         if (rc) {
@@ -1494,7 +1466,7 @@ extern "C" int tfhe_amd_keyswitch_batch_host(TfheAmdContext *c, int B, const int
 
 // largest batch the host path runs unsliced, i.e. whose key-switch inputs are all in the scratch
 // afterwards (tfhe_api.cpp's variance bookkeeping rounds)
-int tfhe_amd_internal_unsliced_max() { return host_slice() > 0 ? host_slice() : 1 << 30; }
+int tfhe_amd_internal_unsliced_max() { return host_slice(); }
 
 // The extracted samples (key-switch inputs) of this context's last gate batch of at most one
 // round (unsliced host path), halves x B rows of kN words: the Tier-1 API's per-thread-lane mode
@@ -1614,7 +1586,9 @@ extern "C" int tfhe_amd_circuit_run_dev(TfheAmdContext *c, TfheAmdCircuit *circ,
 }
 
 extern "C" int tfhe_amd_set_guard_threshold(double distance) {
-    if (!(distance >= 0.0)) return TFHE_AMD_E_ARG;
+    // stricter than the default only: a threshold above 1/8 would let a rounding error of up to
+    // 1 - threshold escape
+    if (!(distance >= 0.0 && distance <= 0.125)) return TFHE_AMD_E_ARG;
     uint64_t bits;
     memcpy(&bits, &distance, 8);
     g_guard_hi.store((uint32_t)(bits >> 32));

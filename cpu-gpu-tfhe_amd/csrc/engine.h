@@ -26,9 +26,8 @@ struct DeviceKey {
 };
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
-// double2 entries (blind_rotate_v6.hip): the v6 tables, then the radix-16 forward's (v10): 4 uniform
-// pass-1 twiddles and the 256-entry per-lane pass-2 table
-constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64 + 4 + 256;
+// double2 entries (blind_rotate_v6.hip build_v6_twiddles)
+constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64;   // fft_wave.h table map
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -113,7 +112,7 @@ hipError_t launch_bk_to_ntt(const int32_t *d_bk_coef, uint32_t *d_bk_ntt, const 
                             hipStream_t s);
 // Blind rotation + sample extraction for `halves` x B ciphertexts: ciphertext g of half h
 // reads in[h] at index g and writes u[h*B + g] (u_a row stride kN).
-// v2 (register-resident NTT) variants, blind_rotate.hip
+// the NTT-domain key layouts and their twiddle streams (ntt_key.hip), used by the v4 kernels
 void build_v2_twiddles(const NttTables &t, uint2 *tu_f, uint2 *tu_i, uint2 *ts_f, uint2 *ts_i);
 hipError_t launch_bk_v1_to_v2(const uint32_t *d_v1, uint32_t *d_v2, hipStream_t s);
 // v4 (v2 layout, inverse CT + lazy CRT + periodic accumulator), blind_rotate_v4.hip

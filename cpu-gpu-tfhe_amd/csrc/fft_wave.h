@@ -1,7 +1,7 @@
 // fft_wave.h — one wave's share of the fp64 negacyclic FFT external product (v6 blind
 // rotation): complex type, butterflies, the three radix-8 register passes and their LDS
-// transposes, twiddle tables, the mod-2^32 rounding and the key MAC; the radix-16 forward of the
-// opt-in v10.  Design: DESIGN.md §3.1 / §5.4b, emulations: scripts/emu_v6.py, scripts/emu_v10.py.
+// transposes, twiddle tables, the mod-2^32 rounding and the key MAC.  Design: DESIGN.md §3,
+// emulation: scripts/emu_v6.py.
 #pragma once
 #include "engine.h"
 
@@ -24,10 +24,6 @@ constexpr int kTwPost = 1028;
 // post-twist)
 constexpr int kTwSig = 1540;
 constexpr int kTwInvAs = 1604;
-// [1668, 1672) the radix-16 forward's (v10) pass-1 stage-3 twiddles W[3][0, 2, 4, 6] (stages 0..2
-// reuse [0, 4)); [1672, 1928) its pass-2 table in the compact order of kT10P2 below
-constexpr int kTwR16U = 1668;
-constexpr int kTwR16P2 = 1672;
 
 __device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
@@ -129,17 +125,9 @@ __device__ __forceinline__ Cx ld(const double2 *p) {
     const double2 v = *p;
     return Cx{v.x, v.y};
 }
-// FFT-domain key loads.  A/B variants (cache policy of the key stream, which every ciphertext
-// of the launch reads from L2): TFHE_AMD_V6_BK_NT = nontemporal loads (nt: bypass L1)
-__device__ __forceinline__ Cx ld_key(const double2 *p) {
-#ifdef TFHE_AMD_V6_BK_NT
-    typedef double d2v __attribute__((ext_vector_type(2)));
-    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p));
-    return Cx{v.x, v.y};
-#else
-    return ld(p);
-#endif
-}
+// FFT-domain key loads (every ciphertext of the launch reads the key slice from L2; nontemporal
+// loads measured no faster, profiles/README.md)
+__device__ __forceinline__ Cx ld_key(const double2 *p) { return ld(p); }
 __device__ __forceinline__ void st(double2 *p, const Cx &v) { *p = make_double2(v.re, v.im); }
 
 // per-lane twiddles of pass B (k = 0) or C (k = 1)
@@ -256,34 +244,10 @@ __device__ __forceinline__ void fft_fwd_AB(Cx (&x)[NP][8], double2 *X, const dou
         wave_sync();
     }
 }
-// the same with the pass-B twiddles supplied by the caller (v7: read from LDS)
+// the same with the pass-B twiddles supplied by the caller (read from the LDS table)
 template <int NP>
 __device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const Tw4 &tA, const Tw4 &t, int L) {
     pass_fwd<NP>(x, tA.w0, tA.w1, tA.w2a, tA.w2b);
-#if defined(TFHE_AMD_DIAG_PERMFWD)
-    // timing diagnostic (wrong results): the forward A -> B transpose replaced by the cross-lane
-    // work a radix-16 forward would need instead (2 x 32 v_permlane{16,32}_swap on the doubles
-    // + 16 on the digit words), to price that design before building it
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int r = 0; r < 8; r += 2) {
-            unsigned *a = reinterpret_cast<unsigned *>(&x[p][r]);
-            unsigned *b = reinterpret_cast<unsigned *>(&x[p][r + 1]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                auto s16 = __builtin_amdgcn_permlane16_swap(a[k], b[k], false, false);
-                auto s32 = __builtin_amdgcn_permlane32_swap(s16[0], s16[1], false, false);
-                a[k] = s32[0];
-                b[k] = s32[1];
-            }
-            if (r < 4) {
-                auto s = __builtin_amdgcn_permlane32_swap(a[0], b[2], false, false);
-                a[0] = s[0];
-                b[2] = s[1];
-            }
-        }
-#elif !defined(TFHE_AMD_DIAG_NOTRAB) && !defined(TFHE_AMD_DIAG_FWDNOTR)
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         store_A(X, x[p], L);
@@ -291,7 +255,6 @@ __device__ __forceinline__ void fft_fwd_AB_t(Cx (&x)[NP][8], double2 *X, const T
         load_B_ab(X, x[p], L);
         wave_sync();
     }
-#endif
     pass_fwd<NP>(x, t.w0, t.w1, t.w2a, t.w2b);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -306,48 +269,12 @@ __device__ __forceinline__ void fft_fwd_C(Cx (&x)[NP][8], const Tw4 &tC) {
     pass_fwd<NP>(x, tC.w0, tC.w1, tC.w2a, tC.w2b);
 }
 
-// rint(c) mod 2^32 for |c| < 2^82 (c within 1/2 of an integer): k = c rounded to a multiple
-// of 2^32 by the 1.5*2^84 shifter, then c - k + 1.5*2^52 rounds c - k to an integer in the
-// low mantissa word.  All three operations are exact except the final rounding.
-__device__ __forceinline__ uint32_t torus_of(double c) {
-    constexpr double M1 = 0x1.8p84, M12 = 0x1.8p84 + 0x1.8p52;
-    const double s = c + M1;
-    const double t = s - M12;
-    const double y = c - t;
-    return (uint32_t)__double_as_longlong(y);
-}
-
-// rint(c) mod 2^32 with the exactness guard's measurement, in one shifter: y = c + 1.5 * 2^52.
-// For |c| < 2^51, y lies in [2^52, 2^53) (ulp 1), so y rounds c to the nearest integer and the
-// low mantissa word is rint(c) mod 2^32; q = y - 1.5 * 2^52 and c - q are exact, and
-// mx = max(mx, |c - q|) is the rounding distance.  Outside that range (the product bound is
-// |c| <= 2^52; real keys give < 2^48) y's exponent differs and its low word is not rint(c):
-// the high word of y, tracked as hlo = min and hhi = max, must stay in [0x43300000, 0x43400000)
-// or the kernel flags the ciphertext (tests/test_guard.py emulates exactly these operations).
-// 3 fp64 adds, one fp64 max and two integer min / max per coefficient (the previous form: two
-// shifters plus a Fast2Sum error, 5 fp64 ops and a max).  TFHE_AMD_V6_NOGUARD: the shifter
-// alone (A/B builds; exact only while |c| < 2^51).
-constexpr uint32_t kShiftHiLo = 0x43300000u;   // high word of 2^52
-constexpr uint32_t kShiftHiEnd = 0x43400000u;  // high word of 2^53
-__device__ __forceinline__ uint32_t torus_of_chk(double c, double &mx, uint32_t &hlo, uint32_t &hhi) {
-    constexpr double M2 = 0x1.8p52;
-    const double y = c + M2;
-#ifndef TFHE_AMD_V6_NOGUARD
-    const double q = y - M2;
-    mx = __builtin_fmax(mx, __builtin_fabs(c - q));
-    const uint32_t hy = (uint32_t)((unsigned long long)__double_as_longlong(y) >> 32);
-    hlo = hy < hlo ? hy : hlo;
-    hhi = hy > hhi ? hy : hhi;
-#endif
-    return (uint32_t)__double_as_longlong(y);
-}
-
 // The rounding of the default kernel (round 3): the 1/8 rule without the distance arithmetic.  y = c + 1.5 * 2^50
 // has ulp 1/4 while |c| < 2^49, so its low mantissa bits are round(4c): round(4c) = 0 mod 4 iff
 // |c - rint(c)| < 1/8 (ties aside), and mantissa bits 2..33 are then rint(c) mod 2^32.  Per
 // coefficient: one fp64 add, an alignbit, an and-or into `bad`, the min / max of the high word
-// (range: [2^50, 2^51)), instead of 3 fp64 adds and a max (torus_of_chk above, kept for the
-// experimental v8 and the TFHE_AMD_V6_DISTGUARD A/B build).  Real keys give |c| < 2^48 (the
+// (range: [2^50, 2^51)), instead of round 2's 3 fp64 adds and a max per coefficient (the
+// distance itself, with a 1.5 * 2^52 shifter).  Real keys give |c| < 2^48 (the
 // product's sigma is 2^44.4); |c| >= 2^49 falls outside the shifter's binade and is flagged.
 // tests/test_guard.py emulates these operations.
 constexpr uint32_t kQShiftHiLo = 0x43100000u;   // high word of 2^50
@@ -388,16 +315,6 @@ __device__ __forceinline__ void write_ext(uint32_t *E, const uint32_t (&acc)[16]
 
 // BK_i rows 2w, 2w + 1 of output c for this lane: 16 x 16 B, all in flight together
 __device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c) {
-#ifdef TFHE_AMD_DIAG_NOBK
-    // timing diagnostic only (wrong results): no key traffic
-    const double s = 1e-9 * (double)(int)(reinterpret_cast<uintptr_t>(bk) & 0xffff);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        b[0][r] = Cx{s + r, s - c};
-        b[1][r] = Cx{s - r, s + c};
-    }
-    return;
-#endif
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         b[0][r] = ld_key(bk + c * 512 + r * 64);
@@ -461,186 +378,6 @@ __device__ __forceinline__ int t8_src(int e) {
     if (e < kT7InvA + 64) return kTwInvAs + (e - kT7InvA);
     if (e < kT8Sig) return kTwInv + 256 + (e - kT7InvA);
     return kTwSig + (e - kT8Sig);
-}
-
-// ---- the radix-16 forward (v10; scripts/emu_v10.py emulates exactly this data flow)
-// compact LDS table: entries [0, 256) = the pass-2 table (per-lane twiddles, by m = L & 15 or
-// t = L & 31): t4[m] (16), t5[m] (16), t6[q][m] (2 x 16), t7[q][m] (4 x 16), t8[q][t] (4 x 32);
-// [256, 288) unused; from kT7InvB on the v6 compact table (the inverse is v6's)
-constexpr int kT10P2 = 0, kT10T5 = 16, kT10T6 = 32, kT10T7 = 64, kT10T8 = 128, kT10P2Words = 256;
-static_assert(kT10P2Words <= kT7FwdC + 256, "the pass-2 table replaces the forward passes B / C entries");
-__device__ __forceinline__ int t10_src(int e) {
-    if (e < kT10P2Words) return kTwR16P2 + e;
-    if (e < kT7InvB) return 0;
-    return t8_src(e);
-}
-// 64-bit halves exchanged by the cross-lane swaps, one dword at a time
-__device__ __forceinline__ void swap32_cx(Cx &a, Cx &b) {   // v_permlane32_swap vdst = a, src = b
-    const unsigned long long ar = __double_as_longlong(a.re), ai = __double_as_longlong(a.im);
-    const unsigned long long br = __double_as_longlong(b.re), bi = __double_as_longlong(b.im);
-    auto s0 = __builtin_amdgcn_permlane32_swap((unsigned)ar, (unsigned)br, false, false);
-    auto s1 = __builtin_amdgcn_permlane32_swap((unsigned)(ar >> 32), (unsigned)(br >> 32), false, false);
-    auto s2 = __builtin_amdgcn_permlane32_swap((unsigned)ai, (unsigned)bi, false, false);
-    auto s3 = __builtin_amdgcn_permlane32_swap((unsigned)(ai >> 32), (unsigned)(bi >> 32), false, false);
-    a.re = __longlong_as_double((long long)(((unsigned long long)s1[0] << 32) | s0[0]));
-    b.re = __longlong_as_double((long long)(((unsigned long long)s1[1] << 32) | s0[1]));
-    a.im = __longlong_as_double((long long)(((unsigned long long)s3[0] << 32) | s2[0]));
-    b.im = __longlong_as_double((long long)(((unsigned long long)s3[1] << 32) | s2[1]));
-}
-__device__ __forceinline__ void swap16_cx(Cx &a, Cx &b) {   // v_permlane16_swap vdst = a, src = b
-    const unsigned long long ar = __double_as_longlong(a.re), ai = __double_as_longlong(a.im);
-    const unsigned long long br = __double_as_longlong(b.re), bi = __double_as_longlong(b.im);
-    auto s0 = __builtin_amdgcn_permlane16_swap((unsigned)ar, (unsigned)br, false, false);
-    auto s1 = __builtin_amdgcn_permlane16_swap((unsigned)(ar >> 32), (unsigned)(br >> 32), false, false);
-    auto s2 = __builtin_amdgcn_permlane16_swap((unsigned)ai, (unsigned)bi, false, false);
-    auto s3 = __builtin_amdgcn_permlane16_swap((unsigned)(ai >> 32), (unsigned)(bi >> 32), false, false);
-    a.re = __longlong_as_double((long long)(((unsigned long long)s1[0] << 32) | s0[0]));
-    b.re = __longlong_as_double((long long)(((unsigned long long)s1[1] << 32) | s0[1]));
-    a.im = __longlong_as_double((long long)(((unsigned long long)s3[0] << 32) | s2[0]));
-    b.im = __longlong_as_double((long long)(((unsigned long long)s3[1] << 32) | s2[1]));
-}
-// The forward's transpose buffer: per half (digit polynomial) 512 positions at slot n + (n >> 5),
-// conflict-free with the register index in the immediate offset on both sides
-constexpr int kR16Half = 528, kR16Slots = 2 * kR16Half;
-// The lane that holds slot 8 L' + r of layout C after the radix-16 forward
-__device__ __forceinline__ int r16_lane(int L) { return (L >> 5) + 2 * ((L >> 4) & 1) + 4 * (L & 15); }
-// Pass 1 and the transpose.  HI / LO: the digits of coefficients L + 64 r of this wave's
-// accumulator polynomial (r < 16).  The halves split by digit: after one v_permlane32_swap per
-// register the lower lanes hold the high digits of coefficients l + 64 r (HI) and l + 32 + 64 r (LO),
-// the upper lanes the low digits, l = L & 31; so position n = l + 32 r' of the lane's digit
-// polynomial (z_n = a_n + i a_{n + 512}) is Z[2 k] = HI[k] + i HI[k + 8], Z[2 k + 1] = LO[k] +
-// i LO[k + 8].  Pass 1 = stages 0..3 (n bits 8..5 = r' bits 3..0, uniform twiddles: u[0..3] as
-// v6's pass A, u3[0..3] = W[3][0, 2, 4, 6]); then ONE transpose through X (both halves,
-// kR16Slots) to lane (m, b') = (L & 15, (L >> 4) & 1) holding
-// n = b' + 2 r'' + 32 m.
-__device__ __forceinline__ void r16_pass1_transpose(const int32_t (&HI)[16], const int32_t (&LO)[16], Cx (&Z)[16],
-                                                    double2 *X, const Tw4 &u, const Tw4 &u3, int L) {
-    int32_t E[16], O[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        auto s = __builtin_amdgcn_permlane32_swap((unsigned)HI[r], (unsigned)LO[r], false, false);
-        E[r] = (int32_t)s[0];
-        O[r] = (int32_t)s[1];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        Z[2 * k] = Cx{(double)E[k], (double)E[k + 8]};
-        Z[2 * k + 1] = Cx{(double)O[k], (double)O[k + 8]};
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) bf_fwd<false>(Z[r], Z[r + 8], u.w0);                 // stage 0 (bit 8)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {                                                        // stage 1 (bit 7)
-        bf_fwd<false>(Z[r], Z[r + 4], u.w1);
-        bf_fwd<true>(Z[r + 8], Z[r + 12], u.w1);
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {                                                        // stage 2 (bit 6)
-        const Cx &t = b < 2 ? u.w2a : u.w2b;
-        const int r0 = 4 * b;
-        if (b & 1) {
-            bf_fwd<true>(Z[r0], Z[r0 + 2], t);
-            bf_fwd<true>(Z[r0 + 1], Z[r0 + 3], t);
-        } else {
-            bf_fwd<false>(Z[r0], Z[r0 + 2], t);
-            bf_fwd<false>(Z[r0 + 1], Z[r0 + 3], t);
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {                                                        // stage 3 (bit 5)
-        const Cx &t = (b >> 1) == 0 ? u3.w0 : (b >> 1) == 1 ? u3.w1 : (b >> 1) == 2 ? u3.w2a : u3.w2b;
-        if (b & 1) bf_fwd<true>(Z[2 * b], Z[2 * b + 1], t);
-        else bf_fwd<false>(Z[2 * b], Z[2 * b + 1], t);
-    }
-    double2 *Xh = X + (L >> 5) * kR16Half;
-    const int l = L & 31;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) st(Xh + l + 33 * r, Z[r]);
-    wave_sync();
-    const int m = L & 15, b1 = (L >> 4) & 1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Z[r] = ld(Xh + b1 + 33 * m + 2 * r);
-    wave_sync();
-}
-// Pass 2 = stages 4..7 (n bits 4..1 = r'' bits 3..0; per-lane twiddles from the compact table),
-// stage 8 (bit 0 = lane bit 4) through v_permlane16_swap, then the two digits' spectra re-paired
-// in every lane by v_permlane32_swap: D[d][r] = digit d at slot 8 r16_lane(L) + r (layout C)
-__device__ __forceinline__ void r16_pass2(Cx (&Z)[16], Cx (&D)[2][8], const double2 *shtw, int L) {
-    const int m = L & 15, t = L & 31;
-    {
-        const Cx t4 = ld(shtw + kT10P2 + m);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) bf_fwd<false>(Z[r], Z[r + 8], t4);                 // stage 4
-    }
-    {
-        const Cx t5 = ld(shtw + kT10T5 + m);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {                                                    // stage 5
-            bf_fwd<false>(Z[r], Z[r + 4], t5);
-            bf_fwd<true>(Z[r + 8], Z[r + 12], t5);
-        }
-    }
-    {
-        const Cx t6a = ld(shtw + kT10T6 + m), t6b = ld(shtw + kT10T6 + 16 + m);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {                                                    // stage 6
-            const Cx &tw = b < 2 ? t6a : t6b;
-            const int r0 = 4 * b;
-            if (b & 1) {
-                bf_fwd<true>(Z[r0], Z[r0 + 2], tw);
-                bf_fwd<true>(Z[r0 + 1], Z[r0 + 3], tw);
-            } else {
-                bf_fwd<false>(Z[r0], Z[r0 + 2], tw);
-                bf_fwd<false>(Z[r0 + 1], Z[r0 + 3], tw);
-            }
-        }
-    }
-    {
-        Cx t7[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t7[q] = ld(shtw + kT10T7 + 16 * q + m);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {                                                    // stage 7
-            if (b & 1) bf_fwd<true>(Z[2 * b], Z[2 * b + 1], t7[b >> 1]);
-            else bf_fwd<false>(Z[2 * b], Z[2 * b + 1], t7[b >> 1]);
-        }
-    }
-    {
-        Cx t8[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t8[q] = ld(shtw + kT10T8 + 32 * q + t);
-#pragma unroll
-        for (int p = 0; p < 8; ++p) swap16_cx(Z[p], Z[p + 8]);                          // stage 8
-#pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            if (p & 1) bf_fwd<true>(Z[p], Z[p + 8], t8[p >> 1]);
-            else bf_fwd<false>(Z[p], Z[p + 8], t8[p >> 1]);
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            swap32_cx(Z[p + 8 * e], Z[p + 4 + 8 * e]);
-            D[0][e + 2 * p] = Z[p + 8 * e];
-            D[1][e + 2 * p] = Z[p + 4 + 8 * e];
-        }
-}
-// The inverse's C -> B transpose from the radix-16 forward's lane order: position n (k = n >> 3,
-// j = n & 7) at slot 16 k + (j ^ t(k >> 2)), t = bits 1 and 3 of its argument exchanged.  Conflict
-// free both ways: a store group of 16 lanes holds k >> 2 = L & 15 (all 16 values of t), a load
-// group two k's 8 apart (t differs in bit 3).  1024 slots (v10).
-__device__ __forceinline__ int r16_t(int m) { return (m & 5) | ((m >> 2) & 2) | ((m & 2) << 2); }
-__device__ __forceinline__ void store_C16(double2 *X, const Cx (&x)[8], int Lp) {
-    const int a = 16 * Lp + r16_t(Lp >> 2);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) st(X + (a ^ r), x[r]);
-}
-__device__ __forceinline__ void load_B16(const double2 *X, Cx (&x)[8], int L) {
-    const int h = L >> 3;
-    const int b0 = 128 * h + ((L & 7) ^ r16_t(2 * h)), b1 = b0 ^ 1;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] = ld(X + (r < 4 ? b0 : b1) + 16 * r);
 }
 
 __device__ __forceinline__ Tw4 tw7_fwdB(const double2 *t, int L) {

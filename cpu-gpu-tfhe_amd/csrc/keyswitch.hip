@@ -476,13 +476,7 @@ __global__ __launch_bounds__(256) void k_ksk_to_v4(const int32_t *__restrict__ k
 // workgroups (atomic partial sums into zeroed rows) so that more waves are in flight when the
 // batch gives fewer than 2 waves per SIMD (B = 128: 0.162 -> 0.093 ms, 256: 0.169 -> 0.102,
 // 512: 0.172 -> 0.129, 768: 0.217 -> 0.165)
-static int ks_split_max() {
-    static const int v = [] {
-        const char *e = getenv("TFHE_AMD_KS_SPLIT");
-        return e ? atoi(e) : 768;   // 128..768: -28..-43 %; 1024 / 4096: +1..3 % (measured)
-    }();
-    return v;
-}
+static int ks_split_max() { return 768; }   // 128..768: -28..-43 %; 1024 / 4096: +1..3 % (measured)
 // Key switches above the small-batch range run on the int8 MFMA kernel (ks-v5) whenever the
 // context built its key layout, which it does unless TFHE_AMD_KS5=0 (then ks-v4: A/B runs)
 bool ks5_enabled() {
@@ -493,14 +487,8 @@ bool ks5_enabled() {
     return v;
 }
 // key-index split of ks-v5: enough workgroups for about 2 per CU (512 for 256 CUs) when the
-// batch has few M-tiles (TFHE_AMD_KS5_SPLIT = 1, 2, 4 or 8 forces one)
+// batch has few M-tiles
 static int ks5_split(int mtiles) {
-    static const int forced = [] {
-        const char *e = getenv("TFHE_AMD_KS5_SPLIT");
-        const int v = e ? atoi(e) : 0;
-        return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
-    }();
-    if (forced) return forced;
     int sp = 1;
     while (sp < 8 && mtiles * kKs5Nb * sp < 512) sp *= 2;
     return sp;
@@ -540,26 +528,14 @@ static void launch_ks4(const DeviceKey &key, int groups, int count, const P &io,
     }
 }
 
-// largest key-switch count for the fully unrolled small kernel (TFHE_AMD_KS_UNROLL overrides):
-// B = 1 0.028 -> 0.021 ms; at B = 8 the 2-way unroll is already faster (0.029 vs 0.031 ms)
-static int ks_unroll_max() {
-    static const int v = [] {
-        const char *e = getenv("TFHE_AMD_KS_UNROLL");
-        return e ? atoi(e) : 4;
-    }();
-    return v;
-}
+// largest key-switch count for the fully unrolled small kernel: B = 1 0.028 -> 0.021 ms; at B = 8
+// the 2-way unroll is already faster (0.029 vs 0.031 ms)
+static int ks_unroll_max() { return 4; }
 
-// largest key-switch count that takes the small-batch kernels (TFHE_AMD_KS_SMALL overrides)
-static int ks_small_max() {
-    static const int v = [] {
-        const char *e = getenv("TFHE_AMD_KS_SMALL");
-        // crossover with ks-v5 (split 8: 0.036 ms flat up to 256) between 12 and 16 (B = 16:
-        // 0.039 vs 0.036 ms, B = 1: 0.021 vs 0.036); with ks-v4 (TFHE_AMD_KS5=0) between 64 and 128
-        return e ? atoi(e) : (ks5_enabled() ? 12 : 96);
-    }();
-    return v;
-}
+// largest key-switch count that takes the small-batch kernels: the crossover with ks-v5 (split 8:
+// 0.036 ms flat up to 256) lies between 12 and 16 (B = 16: 0.039 vs 0.036 ms, B = 1: 0.021 vs
+// 0.036); with ks-v4 (TFHE_AMD_KS5=0) between 64 and 128
+static int ks_small_max() { return ks5_enabled() ? 12 : 96; }
 
 hipError_t launch_keyswitch_rows(const DeviceKey &key, int B, int nks, const CircKs *ks, const int32_t *u_a,
                                  const int32_t *u_b, int32_t *wa, int32_t *wb, hipStream_t s) {
@@ -700,15 +676,7 @@ hipError_t launch_ksk_to_v4(const int32_t *d_ksk, int32_t *d_ksk4, hipStream_t s
 
 // key-switch generation for batches above the small-batch range: 5 (int8 MFMA, the default),
 // 4 (TFHE_AMD_KS5=0)
-int ks_version() {
-    static const int v = [] {
-        const char *e = getenv("TFHE_AMD_KS");
-        const int x = e ? atoi(e) : 4;
-        (void)x;   // 4 / 5; the earlier generations ks-v1 .. v3 were retired in round 4
-        return ks5_enabled() ? 5 : 4;
-    }();
-    return v;
-}
+int ks_version() { return ks5_enabled() ? 5 : 4; }   // ks-v1 .. v3 were retired in round 4
 
 hipError_t launch_keyswitch(const DeviceKey &key, int B, const int32_t *u_a, const int32_t *u_b,
                             const int32_t *u2_a, const int32_t *u2_b, int32_t add_b,

@@ -123,17 +123,9 @@ extern "C" int tfhe_amd_multi_create_raw(const int32_t *bk, const int32_t *ksk, 
     for (int i = 0; i < ndev; ++i) m->workers.emplace_back(new Worker());
     // slot 0's key is uploaded and converted on its device; the other slots copy slot 0's converted
     // key device to device (peer copies over xGMI, concurrently, one worker per slot: SURVEY.md §5).
-    // TFHE_AMD_MULTI_REPLICA=0: every slot uploads and converts its own (the round-3 path).
-    static const bool replicate = [] {
-        const char *e = getenv("TFHE_AMD_MULTI_REPLICA");
-        return !(e && e[0] == '0');
-    }();
     int rc = tfhe_amd_context_create_raw(bk, ksk, m->devices[0], &m->ctx[0]);
     for (int i = 1; i < ndev && rc == TFHE_AMD_OK; ++i)
-        m->workers[i]->submit([=] {
-            return replicate ? tfhe_amd_context_create_replica(m->ctx[0], m->devices[i], &m->ctx[i])
-                             : tfhe_amd_context_create_raw(bk, ksk, m->devices[i], &m->ctx[i]);
-        });
+        m->workers[i]->submit([=] { return tfhe_amd_context_create_replica(m->ctx[0], m->devices[i], &m->ctx[i]); });
     for (int i = 1; i < ndev && m->ctx[0]; ++i) {
         const int r = m->workers[i]->wait();
         if (r != TFHE_AMD_OK && rc == TFHE_AMD_OK) rc = r;

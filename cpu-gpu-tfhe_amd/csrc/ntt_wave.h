@@ -1,5 +1,5 @@
 // ntt_wave.h — register-resident negacyclic NTT building blocks shared by the blind-rotation
-// kernels (blind_rotate.hip v2/v3, blind_rotate_v4.hip).  One wave holds one 1024-point
+// kernels (blind_rotate_v4.hip; key layouts in ntt_key.hip).  One wave holds one 1024-point
 // polynomial as 16 values per lane in three layouts
 //   A: lane L, reg r <-> j = L + 64 r          (wave-uniform twiddles: SGPRs)
 //   B: j = (L & 3) | r << 2 | (L >> 2) << 6

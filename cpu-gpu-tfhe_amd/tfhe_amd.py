@@ -153,7 +153,7 @@ def fp64_ceiling(device=0, waves_per_simd=2, seconds=2.0):
 
 def set_guard_threshold(distance):
     """tfhe_amd_set_guard_threshold: rounding distance at which the fp64 kernel's results are
-    recomputed by the exact NTT kernel (default 1/4; 0 recomputes everything)."""
+    recomputed by the exact NTT kernel (default 1/8, the loosest allowed; 0 recomputes everything)."""
     _check(lib.tfhe_amd_set_guard_threshold(float(distance)), "set_guard_threshold")
 
 
@@ -445,13 +445,17 @@ class Context:
     # ---- host (numpy) batches
     def gate_host(self, gate, ca_a, ca_b, cb_a, cb_b, cc_a=None, cc_b=None, out=None):
         """tfhe_amd_gate_batch_host; out = (r_a [B][500], r_b [B]) int32 arrays to reuse (else new ones).
-        With every array pinned (host_empty / host_copy) the call DMAs straight from and into them."""
+        With every array pinned (host_empty / host_copy) the kernels read the inputs in place and the
+        results are copied straight into `out`.  `out` must be C-contiguous: the library writes B x 500
+        consecutive words (a strided view would be overwritten past its rows)."""
         g = GATES[gate] if isinstance(gate, str) else int(gate)
         ca_a = i32(ca_a); B = ca_a.shape[0]
         if out is not None:
             r_a, r_b = out
             if r_a.shape != (B, n_lwe) or r_b.shape != (B,) or r_a.dtype != np.int32 or r_b.dtype != np.int32:
                 raise TfheAmdError("out: need int32 arrays [B][500] and [B]")
+            if not (r_a.flags["C_CONTIGUOUS"] and r_b.flags["C_CONTIGUOUS"]):
+                raise TfheAmdError("out: need C-contiguous arrays")
         else:
             r_a = np.zeros((B, n_lwe), np.int32); r_b = np.zeros(B, np.int32)
         _check(lib.tfhe_amd_gate_batch_host(self.h, g, B, _p(r_a), _p(r_b), _p(ca_a), _p(i32(ca_b)),

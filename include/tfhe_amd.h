@@ -92,11 +92,14 @@ int tfhe_amd_gate_batch_host(TfheAmdContext *ctx, int gate, int B,
                              const int32_t *cb_a, const int32_t *cb_b,
                              const int32_t *cc_a, const int32_t *cc_b);
 
-/* Caller-owned pinned host buffers (page-locked, portable to every device).  When every array of a
- * tfhe_amd_gate_batch_host call lies inside buffers from tfhe_amd_host_alloc, the call skips the
- * library's pinned staging: its inputs are copied by DMA straight from the caller's arrays and the
- * results straight into them (the reference's per-gate cudaMemcpy pairs, boot-gates.cu:2489-2615,
- * become one DMA per array, overlapped with the previous slice's blind rotation above one round).
+/* Caller-owned pinned host buffers (page-locked, portable to every device and mapped into every
+ * device's address space at the host address; tfhe_amd_host_alloc checks that and returns NULL
+ * otherwise).  When every array of a tfhe_amd_gate_batch_host call lies inside buffers from
+ * tfhe_amd_host_alloc, the call skips the library's pinned staging: the blind rotation's gate
+ * prologue reads the inputs in place over PCIe (zero-copy, no input copy at all), the key switch
+ * writes the results to device memory and one DMA per array copies them straight into the caller's
+ * arrays, overlapped with the next slice's blind rotation above one round (the reference's per-gate
+ * cudaMemcpy pairs, boot-gates.cu:2489-2615, become one DMA per result array).
  * Only the library's own allocations are recognised, so a freed and reused address is never
  * mistaken for pinned memory.  tfhe_amd_host_free returns TFHE_AMD_E_ARG for a pointer that is not
  * the start of a live buffer; tfhe_amd_host_is_pinned reports whether [p, p + bytes) lies in one. */
@@ -287,7 +290,9 @@ int tfhe_amd_last_kernels(TfheAmdContext *ctx, char *buf, int cap);
  * distance 0.06-0.08, FFT errors of one step spread over all its coefficients).  guard_stats reads (and optionally resets)
  * the context's largest distance over the sampled coefficients (one per lane and CMux step) and
  * its count of recomputed ciphertexts (it synchronizes the device).  set_guard_threshold is
- * process-wide (0 recomputes everything: tests; thresholds above 1/8 leave the 1/8 check). */
+ * process-wide and can only make the guard stricter: 0 <= distance <= 1/8 (0 recomputes
+ * everything: tests), anything else returns TFHE_AMD_E_ARG.  There is no way to turn the guard
+ * off. */
 int tfhe_amd_guard_stats(TfheAmdContext *ctx, double *max_distance, long long *recomputed, int reset);
 int tfhe_amd_set_guard_threshold(double distance);
 

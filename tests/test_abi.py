@@ -216,3 +216,17 @@ def test_pinned_arrays_without_gpu_fail_loudly():
         return
     with pytest.raises(T.TfheAmdError):
         T.host_empty((4, 500))
+
+
+def test_gate_host_refuses_strided_out():
+    """A strided view as `out` (e.g. host_empty((B, 1000))[:, :500]) passes the shape and dtype checks
+    but not contiguity: the library writes B x 500 consecutive words, so the binding refuses it
+    before any library call."""
+    B = 4
+    a = np.zeros((B, 500), np.int32)
+    b = np.zeros(B, np.int32)
+    wide = np.zeros((B, 1000), np.int32)
+    with pytest.raises(T.TfheAmdError, match="C-contiguous"):
+        T.Context.gate_host(object(), "NAND", a, b, a, b, out=(wide[:, :500], np.zeros(B, np.int32)))
+    with pytest.raises(T.TfheAmdError, match="C-contiguous"):
+        T.Context.gate_host(object(), "NAND", a, b, a, b, out=(np.zeros((B, 500), np.int32), np.zeros(2 * B, np.int32)[::2]))

@@ -27,7 +27,7 @@ def test_bench_help_runs_without_gpu():
 def test_bench_line_fields():
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "2",
            "--no-clock", "--no-ceiling", "--extra-batches", "none", "--strong-batch", "0", "--host-batches", "none",
-           "--cpu-seconds", "1"]
+           "--no-circuits", "--cpu-seconds", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     d = _line(r.stdout)

@@ -98,23 +98,3 @@ def test_register_rotation_equals_negacyclic_rotation(rng):
             list(rng.integers(0, 2049, 64)):
         want = ext[(np.arange(1024) - a) % 2048]        # (X^a ACC)[j] = E[(j - a) mod 2N]
         assert np.array_equal(_rotate_rreg(acc, int(a)), want), a
-
-
-def test_radix16_forward_matches_v6_forward():
-    """The v10 radix-16 forward (scripts/emu_v10.py: digit split over the wave's halves with
-    v_permlane32_swap, one conflict-free LDS transpose, the last stage across lanes 16 apart, the
-    digits re-paired per lane) gives v6's spectrum at slot 8 L' + r, L' = (L >> 5) + 2 ((L >> 4) & 1)
-    + 4 (L & 15); the inverse's C16 transpose from that lane order is conflict-free too."""
-    import emu_v10 as E10
-    T = E.tables()
-    r = np.random.default_rng(16)
-    for hi, lo in ((r.integers(-512, 512, 1024), r.integers(-512, 512, 1024)),
-                   (np.full(1024, -512), np.full(1024, 511))):
-        D = E10.forward_v10(hi, lo)
-        Lp = E10.logical_lane(np.arange(64))
-        for d, poly in enumerate((hi, lo)):
-            ref = np.empty(512, dtype=complex)
-            ref[E.IDX_C] = E.fwd(poly.astype(float), T)
-            for k in range(8):
-                assert np.max(np.abs(D[:, d, k] - ref[8 * Lp + k])) < 1e-6
-    E10.check_inverse_c16()

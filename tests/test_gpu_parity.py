@@ -270,6 +270,39 @@ def test_host_batch_slices(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
+def test_host_trace_subprocess(keyset, rng, tmp_path):
+    """TFHE_AMD_HOST_TRACE=1 (read once per process): one stderr line per host-pointer batch call with
+    its host-side phases (staged, sliced and pinned paths), and the results are unchanged."""
+    import subprocess
+    import sys
+    x, y = rng.integers(0, 2, 1100), rng.integers(0, 2, 1100)
+    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
+    np.savez(tmp_path / "in.npz", a_a=a_a, a_b=a_b, b_a=b_a, b_b=b_b, x=x, y=y)
+    code = r"""
+import sys, numpy as np
+sys.path[:0] = [%r]
+import tfhe_amd as T
+K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); z = np.load(%r)
+for B in (64, 1100):
+    r = c.gate_host("NAND", z["a_a"][:B], z["a_b"][:B], z["b_a"][:B], z["b_b"][:B])
+    assert np.array_equal(K.decrypt(*r), 1 - (z["x"][:B] & z["y"][:B]))
+pin = [T.host_copy(z[k][:64]) for k in ("a_a", "a_b", "b_a", "b_b")]
+r = c.gate_host("NAND", *pin, out=(T.host_empty((64, 500)), T.host_empty(64)))
+assert np.array_equal(K.decrypt(*r), 1 - (z["x"][:64] & z["y"][:64]))
+print("trace ok")
+""" % (os.path.join(REPO, "cpu-gpu-tfhe_amd"), str(tmp_path / "in.npz"))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, TFHE_AMD_HOST_TRACE="1"),
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "trace ok" in r.stdout, r.stdout + r.stderr
+    lines = [ln for ln in r.stderr.splitlines() if ln.startswith("host_trace ")]
+    assert len(lines) >= 3, r.stderr[-2000:]
+    assert any("B=64" in ln for ln in lines) and any("B=1100" in ln for ln in lines)
+    assert any(ln.startswith("host_trace pinned ") for ln in lines), lines
+    for ln in lines:
+        f = dict(kv.split("=") for kv in ln.split()[2:])
+        assert float(f["total"]) > 0.0 and all(float(v) >= 0.0 for v in f.values()), ln
+
+
 @pytest.mark.parametrize("gate,B", [("NAND", 64), ("NAND", 1024), ("MUX", 2100), ("AND", 777)])
 def test_pinned_host_batch_equals_device_path(ctx, okey, keyset, rng, gate, B):
     """Caller-owned pinned arrays (tfhe_amd_host_alloc via T.host_copy / host_empty): the host call
@@ -469,61 +502,6 @@ print("barrier ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "barrier ok" in r.stdout
-
-
-@pytest.mark.parametrize("mode,batches", [
-    ("1", (("NAND", 1100), ("AND", 777), ("MUX", 700))),
-    ("2", (("NAND", 1), ("XOR", 50), ("MUX", 150), ("OR", 385))),
-])
-def test_radix16_v10_subprocess(ctx, keyset, rng, tmp_path, mode, batches):
-    """TFHE_AMD_V10 (read once per process) runs the radix-16 forward.  Mode 1, the throughput
-    launches (> 2 CUs ciphertexts) through k_blind_rotate_v10: a 1100-gate NAND batch (a full 1024
-    launch and a v6 remainder), a 777-gate AND batch (odd: a padding ciphertext) and a 700-gate
-    MUX batch (1400 rotations).  Mode 2, every launch: one ciphertext per workgroup (v10s) at
-    B = 1 / 50, paired at 300 MUX rotations and 385 gates.  All equal the default path word for
-    word, the oracle on sampled gates, with no ciphertext handed to the guard's exact
-    recomputation."""
-    import subprocess
-    import sys
-    sets = []
-    for gate, B in batches:
-        k = 3 if gate == "MUX" else 2
-        vals = [rng.integers(0, 2, B) for _ in range(k)]
-        cts = [keyset.encrypt(v, rng) for v in vals]
-        sets.append((gate, [x for ab in cts for x in ab]))
-    inp = tmp_path / "in.npz"
-    np.savez(inp, **{f"{g}_{i}": a for g, arrs in sets for i, a in enumerate(arrs)})
-    out = tmp_path / "out.npz"
-    code = r"""
-import sys, numpy as np
-sys.path[:0] = [%r, %r]
-import tfhe_amd as T, oracle_ctypes as O
-K = T.SecretKeyset(); c = T.Context(K.bk, K.ksk, device=0); o = O.OracleKey(K.bk, K.ksk)
-z = np.load(%r); res = {}
-c.guard_stats(reset=True)
-for gate, k in %r:
-    arrs = [z[f"{gate}_{i}"] for i in range(k)]
-    r = c.gate_host(gate, *arrs)
-    assert any("v10" in x for x in c.last_kernels()), c.last_kernels()
-    res[gate + "_a"], res[gate + "_b"] = r
-    B = len(arrs[1]); idx = np.array(sorted({i for i in (0, 1, 510, 511, 512, B // 2, B - 2, B - 1) if 0 <= i < B}))
-    w = o.gate_batch(gate, *[a[idx] for a in arrs])
-    assert np.array_equal(r[0][idx], w[0]) and np.array_equal(r[1][idx], w[1]), gate
-dist, redo = c.guard_stats()
-assert redo == 0, (dist, redo)
-np.savez(%r, **res)
-print("v10 ok", dist)
-""" % (os.path.join(REPO, "cpu-gpu-tfhe_amd"), os.path.join(REPO, "tests"), str(inp),
-       tuple((g, len(a)) for g, a in sets), str(out))
-    env = dict(os.environ, TFHE_AMD_V10=mode)
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "v10 ok" in r.stdout
-    got = np.load(out)
-    for gate, arrs in sets:
-        ra, rb = ctx.gate_host(gate, *arrs)
-        assert not any("v10" in x for x in ctx.last_kernels())
-        assert np.array_equal(got[gate + "_a"], ra) and np.array_equal(got[gate + "_b"], rb), gate
 
 
 def test_fp64_ceiling_measurement():

@@ -216,72 +216,77 @@ def test_quarter_shifter_rounding_exact_or_flagged():
     assert flagged.sum() > 5000 and (~flagged).sum() > 5000
 
 
-_ADV = r"""
-import sys, json, numpy as np
-sys.path[:0] = [%r, %r]
-import tfhe_amd as T
-K = T.SecretKeyset()
-rng = np.random.default_rng(31)
-sh = K.bk.shape
-keys = {
-    # random magnitudes in (2^31 - 2^16, 2^31), all positive
-    "allpos16": ((2**31 - 1) - rng.integers(0, 2**16, size=sh, dtype=np.int64)).astype(np.int32),
-    # a random high-magnitude constant and a random sign per polynomial
-    "polyconst": np.broadcast_to(rng.choice([-1, 1], size=sh[:-1] + (1,)) *
-                                 rng.integers(2**31 - 2**24, 2**31, size=sh[:-1] + (1,)), sh).astype(np.int32),
-}
-B = 64
-x_a = rng.integers(-2**31, 2**31, (B, 500), dtype=np.int64).astype(np.int32)
-x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
-out = {}
-for name, bk in keys.items():
-    c = T.Context(bk, K.ksk, device=0)
-    u = c.woks_host(T.MU, x_a, x_b)
-    d, r = c.guard_stats()
-    c.close()
-    np.save(sys.argv[1] + "/" + name + "_a.npy", u[0]); np.save(sys.argv[1] + "/" + name + "_b.npy", u[1])
-    np.save(sys.argv[1] + "/" + name + "_bk.npy", bk)
-    out[name] = [d, r]
-np.save(sys.argv[1] + "/x_a.npy", x_a); np.save(sys.argv[1] + "/x_b.npy", x_b); np.save(sys.argv[1] + "/ksk.npy", K.ksk)
-print(json.dumps(out))
-"""
+def _adversarial_keys(shape, rng):
+    return {
+        # random magnitudes in (2^31 - 2^16, 2^31), all positive
+        "allpos16": ((2**31 - 1) - rng.integers(0, 2**16, size=shape, dtype=np.int64)).astype(np.int32),
+        # a random high-magnitude constant and a random sign per polynomial
+        "polyconst": np.broadcast_to(rng.choice([-1, 1], size=shape[:-1] + (1,)) *
+                                     rng.integers(2**31 - 2**24, 2**31, size=shape[:-1] + (1,)),
+                                     shape).astype(np.int32),
+    }
 
 
-def _adv_run(tmp, guard):
-    import json
-    import subprocess
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = _ADV % (os.path.join(repo, "cpu-gpu-tfhe_amd"), os.path.join(repo, "tests"))
-    env = dict(os.environ)
-    if not guard:
-        env["TFHE_AMD_GUARD"] = "0"
-    r = subprocess.run([sys.executable, "-c", code, str(tmp)], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout + r.stderr
-    return json.loads(r.stdout.strip().splitlines()[-1])
+def _raw_fp64_woks(c, x_a, x_b):
+    """The woKS bootstrap through the raw fp64 CMux steps (tfhe_amd_blind_rotate_dev: the v6 step
+    kernel with no exactness guard — the library's only unguarded entry, a kernel-test API) and the
+    sample extraction in numpy: what the fp64 kernel computes when nothing checks its rounding.
+    ACC = (0, X^{2N - barb} (mu, ..., mu)) (lwe-bootstrapping-functions-fft.cu:1427-1431), 500 steps
+    with bara_i = modSwitchFromTorus32(x_a[i], 2N), u.a[j] = -acc_a[N - j], u.b = acc_b[0] (lwe.cu:41-56)."""
+    import torch
+    B = x_a.shape[0]
+    acc = np.zeros((B, 2, 1024), np.int32)
+    bara = np.zeros((B, 500), np.int32)
+    tv = np.full(1024, T.MU, np.int32)
+    for k in range(B):
+        acc[k, 1] = O.mul_by_xai(2048 - O.modswitch_from(int(x_b[k]), 2048), tv)
+        bara[k] = [O.modswitch_from(int(v), 2048) for v in x_a[k]]
+    d_acc = torch.from_numpy(acc).cuda()
+    c.blind_rotate_dev(d_acc, torch.from_numpy(bara).cuda(), 500)
+    c.sync()
+    r = d_acc.cpu().numpy().astype(np.int64)
+    u_a = np.concatenate([r[:, 0, :1], -r[:, 0, :0:-1]], axis=1)
+    return O.i32(u_a), O.i32(r[:, 1, 0])
 
 
 @pytest.mark.gpu
-def test_guard_random_adversarial_keys(tmp_path):
+def test_guard_random_adversarial_keys(keyset):
     """Random high-magnitude keys (not constant: random magnitudes near 2^31, or a random constant
-    and sign per polynomial) push the fp64 FFT error across 1/2 on some ciphertexts: without the
-    guard (TFHE_AMD_GUARD=0, a subprocess) some of the 64 woKS outputs differ from the exact
-    oracle; with it (the default) the guard flags them and every output equals the oracle."""
-    (tmp_path / "g").mkdir()
-    (tmp_path / "u").mkdir()
-    stats = _adv_run(tmp_path / "g", True)
-    _adv_run(tmp_path / "u", False)
-    ld = lambda d, n: np.load(str(tmp_path / d / n))
-    x_a, x_b, ksk = ld("g", "x_a.npy"), ld("g", "x_b.npy"), ld("g", "ksk.npy")
+    and sign per polynomial) push the fp64 FFT error across 1/2 on some ciphertexts: through the
+    raw, unguarded fp64 steps some of the 64 woKS outputs differ from the exact oracle; through the
+    product's woKS call (guarded; the guard cannot be turned off) the guard flags them and every
+    output equals the oracle."""
+    rng = np.random.default_rng(31)
+    keys = _adversarial_keys(keyset.bk.shape, rng)
+    B = 64
+    x_a = rng.integers(-2**31, 2**31, (B, 500), dtype=np.int64).astype(np.int32)
+    x_b = rng.integers(-2**31, 2**31, B, dtype=np.int64).astype(np.int32)
     report = {}
-    for name in ("allpos16", "polyconst"):
-        bk = ld("g", name + "_bk.npy")
-        want = O.OracleKey(bk, ksk, use_ntt=True).woks_batch(T.MU, x_a, x_b, nthreads=8)
-        wrong = lambda d: int(np.sum(np.any(ld(d, name + "_a.npy") != want[0], axis=1) | (ld(d, name + "_b.npy") != want[1])))
-        report[name] = {"guard_distance": stats[name][0], "recomputed": stats[name][1],
-                        "wrong_unguarded": wrong("u"), "wrong_guarded": wrong("g")}
+    for name, bk in keys.items():
+        c = T.Context(bk, keyset.ksk, device=0)
+        try:
+            g = c.woks_host(T.MU, x_a, x_b)
+            d, redo = c.guard_stats()
+            u = _raw_fp64_woks(c, x_a, x_b)
+        finally:
+            c.close()
+        want = O.OracleKey(bk, keyset.ksk, use_ntt=True).woks_batch(T.MU, x_a, x_b, nthreads=8)
+        wrong = lambda r: int(np.sum(np.any(r[0] != want[0], axis=1) | (r[1] != want[1])))
+        report[name] = {"guard_distance": d, "recomputed": redo, "wrong_unguarded": wrong(u),
+                        "wrong_guarded": wrong(g)}
     print(report)
     for name, r in report.items():
         assert r["wrong_guarded"] == 0, (name, r)
         assert r["recomputed"] >= r["wrong_unguarded"], (name, r)
         assert r["guard_distance"] >= 0.125, (name, r)
     assert sum(r["wrong_unguarded"] for r in report.values()) > 0, report   # the errors do cross 1/2
+
+
+def test_guard_threshold_can_only_tighten():
+    """tfhe_amd_set_guard_threshold accepts 0 .. 1/8 and refuses anything looser: no call turns the
+    exactness guard off."""
+    for bad in (0.1251, 0.5, 1.0, -0.1, float("nan")):
+        with pytest.raises(T.TfheAmdError):
+            T.set_guard_threshold(bad)
+    T.set_guard_threshold(0.0)
+    T.set_guard_threshold(0.125)

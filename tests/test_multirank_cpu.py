@@ -231,8 +231,9 @@ def _ranks_worker(rank, world, port, mode, out):
     bench.device_identity = lambda torch, local: {"device": dev, "name": "stub", "cus": 256,
                                                   "pci": "0000:%02x:00" % pci, "uuid": "GPU-%d" % dev}
     parity = {"checked_per_rank": 128, "mismatches": 0, "mismatches_local": rank}
-    blk = bench.rank_block(dist, None, rank, "gloo", rank, world, True, parity, rank == 0, 3.0 + rank)
-    blk_nccl = bench.rank_block(dist, None, rank, "nccl", rank, world, True, parity, True, 3.0)
+    strong_ok = {"1024": rank == 0, "4096": True}
+    blk = bench.rank_block(dist, None, rank, "gloo", rank, world, True, parity, strong_ok, 3.0 + rank)
+    blk_nccl = bench.rank_block(dist, None, rank, "nccl", rank, world, True, parity, strong_ok, 3.0)
     out.put((rank, blk, blk_nccl["distinct_devices"]))
     dist.barrier()
     dist.destroy_process_group()
@@ -255,5 +256,6 @@ def test_two_rank_bench_ranks_block(mode):
         assert blk["world_size"] == 2 and blk["backend"] == "gloo"
         assert [r["rank"] for r in blk["per_rank"]] == [0, 1]
         assert [r["parity_mismatches_local"] for r in blk["per_rank"]] == [0, 1]
-        assert [r["strong_truth_table_ok"] for r in blk["per_rank"]] == [True, False]
+        assert [r["strong_truth_table_ok"]["1024"] for r in blk["per_rank"]] == [True, False]
+        assert [r["strong_truth_table_ok"]["4096"] for r in blk["per_rank"]] == [True, True]
         assert blk["distinct_devices"] == (mode != "same") == distinct_nccl

@@ -45,6 +45,7 @@ inline uint2 make_uint2(unsigned x, unsigned y) { return uint2{x, y}; }
 #define hipEventDisableTiming 2
 #define hipHostMallocDefault 0
 #define hipHostMallocPortable 1
+#define hipHostMallocMapped 2
 
 // one in-order queue of device work, run by its own thread
 struct StubStream {
@@ -140,6 +141,8 @@ template <class T> inline hipError_t hipMalloc(T **p, size_t n) { return hipMall
 inline hipError_t hipFree(void *p) { free(p); return hipSuccess; }
 inline hipError_t hipHostMalloc(void **p, size_t n, unsigned) { return hipMalloc(p, n); }
 template <class T> inline hipError_t hipHostMalloc(T **p, size_t n, unsigned f) { return hipHostMalloc((void **)p, n, f); }
+// host memory is the device's in the stand-in: mapped at the same address
+inline hipError_t hipHostGetDevicePointer(void **dp, void *p, unsigned) { *dp = p; return hipSuccess; }
 inline hipError_t hipHostFree(void *p) { free(p); return hipSuccess; }
 inline hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind) { if (n) memmove(d, s, n); return hipSuccess; }
 inline hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind, hipStream_t st) {
