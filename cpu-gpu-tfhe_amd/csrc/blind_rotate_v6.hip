@@ -153,7 +153,8 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     double2 *X = sh.X[own];
     uint32_t *E = reinterpret_cast<uint32_t *>(X);
     V6_STAMP(9);
-    const double2 *bk = g.bk + ((size_t)i * 8 + (size_t)w * 4) * 512 + L;
+    const __amdgpu_buffer_rsrc_t rk = key_rsrc(g.bk);
+    const int row0 = i * 8 + w * 4;   // rows (2w, 2w + 1) of slice i, wave-uniform
     Cx bv[2][8];                  // 16 key loads in flight (256-VGPR budget: 2 waves per SIMD)
     // (X^a - 1) ACC_w and its signed gadget digits (tgsw-functions.cu:300-413):
     // hi = sext10 bits 22..31 of diff + off + 2^31, lo = sext10 bits 12..21 of diff + off + 2^21
@@ -252,13 +253,13 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     // VGPRs live across the step, measured slower: B = 512 2.336 vs 2.273 ms, profiles/r04f_*)
     {
         const Tw4 tC = tw7_fwdC(shtw, L);
-        load_bk(bv, bk, 1 - w);
+        load_bk(bv, rk, row0, 1 - w, L);
         __builtin_amdgcn_sched_barrier(0);   // keep the 16 loads issued ahead of pass C
         fft_fwd_C<2>(D, tC);
     }
     mac6(D, bv, Y);
     V6_STAMP(2);
-    load_bk(bv, bk, w);
+    load_bk(bv, rk, row0, w, L);
     __builtin_amdgcn_sched_barrier(0);
     store_C(X, Y, L);
     // the second MAC runs after the barrier and the partner-partial loads, so that its key
@@ -343,7 +344,9 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
     // rounding distance for the exactness guard
     // the 1/8 rule on every coefficient through the quarter-ulp shifter (bad, fft_wave.h
     // torus_of_qchk: B = 1 024 / 4 096 -0.9 / -1.1 %, profiles/r03_qguard_ab.txt); the distance
-    // itself on one coefficient per lane and step, for the statistic (tfhe_amd_guard_stats)
+    // itself on one coefficient per lane and step, for the statistic (tfhe_amd_guard_stats; sampling
+    // it every fourth step instead saves 3 fp64 per wave-step only with a real branch, which splits
+    // the inverse's tail from the rounding)
     mx = __builtin_fmax(mx, __builtin_fabs(Y[0].re - __builtin_rint(Y[0].re)));
 #pragma unroll
     for (int r = 0; r < 8; ++r) {

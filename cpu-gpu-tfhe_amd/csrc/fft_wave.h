@@ -125,9 +125,6 @@ __device__ __forceinline__ Cx ld(const double2 *p) {
     const double2 v = *p;
     return Cx{v.x, v.y};
 }
-// FFT-domain key loads (every ciphertext of the launch reads the key slice from L2; nontemporal
-// loads measured no faster, profiles/README.md)
-__device__ __forceinline__ Cx ld_key(const double2 *p) { return ld(p); }
 __device__ __forceinline__ void st(double2 *p, const Cx &v) { *p = make_double2(v.re, v.im); }
 
 // per-lane twiddles of pass B (k = 0) or C (k = 1)
@@ -313,13 +310,32 @@ __device__ __forceinline__ void write_ext(uint32_t *E, const uint32_t (&acc)[16]
     for (int r = 0; r < 16; ++r) e6_store(E, L + 64 * r, acc[r], r < 3);
 }
 
-// BK_i rows 2w, 2w + 1 of output c for this lane: 16 x 16 B, all in flight together
-__device__ __forceinline__ void load_bk(Cx (&b)[2][8], const double2 *bk, int c) {
+// BK_i rows 2w, 2w + 1 of output c for this lane: 16 x 16 B, all in flight together, as buffer
+// loads: the key is one buffer resource (SGPRs), the slice / row / output offset of each row is
+// wave-uniform (soffset, SGPR) and the lane's offset loop-invariant (voffset, 2 VGPRs + immediate
+// offsets), so a step spends no vector ALU on key addresses (the flat-pointer form recomputed 64-bit
+// lane addresses: 12 VALU per wave-step)
+__device__ __forceinline__ Cx ld_key_buf(__amdgpu_buffer_rsrc_t rk, int voff, int soff) {
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    const i4 v = __builtin_bit_cast(i4, __builtin_amdgcn_raw_buffer_load_b128(rk, voff, soff, 0));
+    const long long lo = ((long long)(unsigned)v.y << 32) | (unsigned)v.x;
+    const long long hi = ((long long)(unsigned)v.w << 32) | (unsigned)v.z;
+    return Cx{__longlong_as_double(lo), __longlong_as_double(hi)};
+}
+// row0 = the key row index (i * 8 + 4 w) of rows (2w, 2w + 1) of slice i, wave-uniform
+__device__ __forceinline__ void load_bk(Cx (&b)[2][8], __amdgpu_buffer_rsrc_t rk, int row0, int c, int L) {
+    const int s0 = __builtin_amdgcn_readfirstlane((row0 + c) * 512 * 16);
+    const int s1 = s0 + 2 * 512 * 16;
+    const int v = L * 16;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-        b[0][r] = ld_key(bk + c * 512 + r * 64);
-        b[1][r] = ld_key(bk + (2 + c) * 512 + r * 64);
+        b[0][r] = ld_key_buf(rk, v + r * 1024, s0);
+        b[1][r] = ld_key_buf(rk, v + r * 1024, s1);
     }
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t key_rsrc(const double2 *bk) {
+    // raw buffer of the whole FFT-domain key (32.8 MB), dword 3 = the gfx9 default format
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double2 *>(bk), 0, 0x7fffffff, 0x00020000);
 }
 // Y = D_0 (x) BK[row 2w][c] + D_1 (x) BK[row 2w + 1][c], layout C
 // Y = o + sum_p D_p b_p: the second MAC seeded with the partner wave's partial sum (its first
