@@ -265,12 +265,9 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
 /* Select the blind-rotation kernel generation: 0 = default (= 6: fp64 FFT external product,
- * the reference's arithmetic, with the exactness guard above), 4 = the exact 2-prime NTT kernel.
- * EXPERIMENTAL=1 builds also carry 1 (LDS radix-2 reference kernel), 2 (register-resident NTT,
- * 2 waves per ciphertext), 3 (4 waves), 5 (8 waves per ciphertext, latency) and 7 (v6 with the
- * key slice shared through LDS).  Returns TFHE_AMD_E_ARG for a generation this build lacks.
- * env TFHE_AMD_BR=<n> does the same at startup.  For A/B measurements and parity
- * cross-checks; results are identical. */
+ * the reference's arithmetic, with the exactness guard above; launches of at most one ciphertext
+ * per CU run its four-wave form v12), 4 = the exact 2-prime NTT kernel for every launch.  Returns
+ * TFHE_AMD_E_ARG for a generation this build lacks.  Process-wide; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
 
 /* The kernels (with the variant the launch geometry picked, e.g. "k_blind_rotate_v6(reg-rotation)",

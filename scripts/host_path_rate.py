@@ -59,7 +59,7 @@ for B in [int(b) for b in (sys.argv[1:] or ["1", "1024", "4096"])]:
     ds = float(np.median(tsync))
     print(json.dumps({"batch": B, "ms_per_call": dt * 1e3, "ms_min": min(ts) * 1e3, "ms_mean": float(np.mean(ts)) * 1e3,
                       "statistic": "median of %d calls" % reps, "gate_bootstraps_per_s": B / dt, "truth_table_ok": ok,
-                      "device_path_ms": dd * 1e3, "device_path_sync_ms": ds * 1e3, "slice": os.environ.get("TFHE_AMD_HOST_SLICE", "1024"),
+                      "device_path_ms": dd * 1e3, "device_path_sync_ms": ds * 1e3, "slice": 1024,
                       "path": "host pointers, caller-owned pinned arrays (DMA straight from and into them)" if PINNED
                       else "host pointers (pinned staging + PCIe both ways)", "engine": T.version()}))
 ctx.close()

@@ -14,11 +14,9 @@ PEAK = 78.6
 
 
 def is_headline_br(name):
-    """the one-ciphertext-per-workgroup fp64 kernel (k_blind_rotate_v6<...>; k_blind_rotate_v10<...>
-    under TFHE_AMD_V10), not the paired /
-    circuit-row / debug forms"""
-    return (("k_blind_rotate_v6<" in name and "v6p" not in name and "v6_rows" not in name and "v6_debug" not in name)
-            or "k_blind_rotate_v10<" in name)
+    """the one-ciphertext-per-workgroup fp64 kernel of the headline (k_blind_rotate_v6<...>), not the
+    paired / four-wave / circuit-row / debug forms"""
+    return "k_blind_rotate_v6<" in name and "v6p" not in name and "v6_rows" not in name and "v6_debug" not in name
 
 
 def main():
