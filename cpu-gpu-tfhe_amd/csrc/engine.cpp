@@ -784,7 +784,7 @@ int tfhe_amd_internal_l1(TfheAmdContext *c, int op, int B, int iters, const int3
 // of the call's 0.3 ms copy overhead and a 4 096-gate batch's 1 ms (scripts/host_copy_ubench.cpp,
 // profiles/r04b_host_copy_ubench.jsonl: 4 threads 0.05 / 0.19 ms).  Copies below 1 MB in all, and
 // calls that find the pool busy (another context copying), run on the caller's thread.
-// TFHE_AMD_COPY_THREADS sets the pool's helper threads (default 3; 0 = no pool).
+// The pool has 3 helper threads.
 struct CopyJob {
     void *dst;
     const void *src;

@@ -23,11 +23,12 @@ else
 fi
 # PMC passes: the same command with --no-clock — amd-smi is a python script started through
 # /usr/bin/env, an exec the box refuses once the PMC profiler's preload has initialised the GPU
-# (round-5 session r05a: the refused execs left the write pass hung)
+# (round-5 session r05a: the refused execs left the write pass hung); and --no-circuits: the PMC
+# summaries read only the headline's launches, which come first
 run() {   # name, extra rocprofv3 args...
   local name=$1; shift
   local extra=""
-  case " $* " in *" --pmc "*) extra="--no-clock" ;; esac
+  case " $* " in *" --pmc "*) extra="--no-clock --no-circuits" ;; esac
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $BENCH $extra > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"

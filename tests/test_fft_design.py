@@ -98,3 +98,36 @@ def test_register_rotation_equals_negacyclic_rotation(rng):
             list(rng.integers(0, 2049, 64)):
         want = ext[(np.arange(1024) - a) % 2048]        # (X^a ACC)[j] = E[(j - a) mod 2N]
         assert np.array_equal(_rotate_rreg(acc, int(a)), want), a
+
+
+def test_four_wave_half_transforms_emulation():
+    """The four-wave kernel (blind_rotate_v12.hip, scripts/emu_v12.py): stage 0 split into halves,
+    four radix-4 passes per half over layouts A' B' C' D', the key read at v6's layout, the DIT
+    inverse inside each half with the lane factor folded into pass A', stage 8 across the halves:
+    v6's spectrum slot for slot and the exact negacyclic product."""
+    import emu_v12
+    emu_v12.main()
+
+
+def test_four_wave_lds_slot_maps_conflict_free():
+    """The slot maps of blind_rotate_v12.hip's transposes (sAB, sBC, sCD): every 16-B store (8-lane
+    groups, 128-B rows) and 16-B load (the four 16-lane groups of ds_read_b128, 256-B rows) of every
+    transpose they serve hits distinct banks (MI355X_MICROARCH.md §LDS), and each map is one to one
+    within its buffer."""
+    lay = {"A": lambda l, r: l + 64 * r, "B": lambda l, r: (l & 15) + 16 * r + 64 * (l >> 4),
+           "C": lambda l, r: (l & 3) + 4 * r + 16 * (l >> 2), "D": lambda l, r: 4 * l + r}
+    sAB = lambda m: m
+    sBC = lambda m: m ^ (((m >> 4) & 3) << 2)
+    sCD = lambda m: m + (m >> 2)
+    wg = [list(range(8 * k, 8 * k + 8)) for k in range(8)]
+    g = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27], [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+    rg = g + [[x + 32 for x in grp] for grp in g]
+    uses = [(sAB, "A", "B"), (sAB, "B", "A"), (sBC, "B", "C"), (sBC, "C", "B"), (sCD, "C", "D"), (sCD, "D", "C"),
+            (sCD, "D", "D"), (sAB, "A", "A")]
+    for f, X, Y in uses:
+        assert len({f(m) for m in range(256)}) == 256 and max(f(m) for m in range(256)) < 320
+        for r in range(4):
+            for grp in wg:
+                assert len({f(lay[X](l, r)) % 8 for l in grp}) == 8, (X, Y, r)
+            for grp in rg:
+                assert len({f(lay[Y](l, r)) % 16 for l in grp}) == 16, (X, Y, r)
