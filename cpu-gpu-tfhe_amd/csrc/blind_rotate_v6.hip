@@ -624,32 +624,6 @@ void build_v6_twiddles(double2 *tw) {
         tw[kTwSig + L] = cexp(L, 2048);                             // zeta^-L
         tw[kTwInvAs + L] = cexp(17 * L, 2048);                      // e^{-2 pi i L / 128} zeta^-L
     }
-    // the four-wave kernel (v12, scripts/emu_v12.py): forward passes B', C', D' of half h, stages
-    // (3, 4), (5, 6), (7, 8) — W[s][b] at the block b of the lane's positions; inverse passes C', B',
-    // A' (DIT twiddles e^{-2 pi i j / 2^(k+1)}, the lane factor zeta^-L folded into A'), stage 8
-    for (int h = 0; h < 2; ++h)
-        for (int L = 0; L < 64; ++L) {
-            double2 *f = tw + kTw12 + h * 6 * 64 + L;
-            f[0 * 64] = cis(W[3][4 * h + (L >> 4)]);
-            f[1 * 64] = cis(W[4][8 * h + 2 * (L >> 4)]);
-            f[2 * 64] = cis(W[5][16 * h + (L >> 2)]);
-            f[3 * 64] = cis(W[6][32 * h + 2 * (L >> 2)]);
-            f[4 * 64] = cis(W[7][64 * h + L]);
-            f[5 * 64] = cis(W[8][128 * h + 2 * L]);
-        }
-    for (int L = 0; L < 64; ++L) {
-        double2 *q = tw + kTw12 + 12 * 64 + L;
-        q[0 * 64] = cexp(L & 3, 8);
-        q[1 * 64] = cexp(L & 3, 16);
-        q[2 * 64] = cexp(L & 15, 32);
-        q[3 * 64] = cexp(L & 15, 64);
-        // e^{-2 pi i L / 128} zeta^-L = e^{-2 pi i 17 L / 2048}
-        q[4 * 64] = cexp(17 * L, 2048);
-        q[5 * 64] = cexp(L, 256);
-        q[6 * 64] = cexp(L, 2048);
-        q[7 * 64] = cexp(L, 512);
-        q[8 * 64] = cexp(L + 64, 512);
-    }
     for (int L = 0; L < 64; ++L) {
         const int g = L >> 3;
         tw[4 + 0 * 64 + L] = cis(W[3][g]);
@@ -706,17 +680,6 @@ static bool v6p_pairsync() {
 // only the ciphertext's own two waves, measured no faster: B = 1 024 3.039 vs 3.010 ms, B = 1 / 64
 // / 256 1.676 / 1.713 / 1.726 vs 1.642 / 1.693 / 1.695 ms — a barrier between two waves in step is
 // cheaper than polling: profiles/r04k_v6_pairsync_ab.txt, r04w_v6_pairsync_small_ab.txt)
-// launches of at most one ciphertext per CU take the four-wave kernel (blind_rotate_v12.hip:
-// two waves per SIMD pair instead of two idle SIMDs); TFHE_AMD_NO_V12 builds the v6-only library
-// (A/B variant builds)
-static bool v12_for(const DeviceKey &key, long n) {
-#ifdef TFHE_AMD_NO_V12
-    (void)key; (void)n;
-    return false;
-#else
-    return n <= v6_cus(key);
-#endif
-}
 static bool v6_rreg(const DeviceKey &key, long n) {
     static const char *env = getenv("TFHE_AMD_V6_RREG");
     if (env) return atoi(env) != 0;
@@ -749,10 +712,7 @@ hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const
     const long total = (long)B * halves, chunk = v6_chunk(key);
     for (long base = 0; base < total; base += chunk) {
         const long n = total - base < chunk ? total - base : chunk;
-        if (v12_for(key, n)) {
-            const hipError_t e = launch_blind_rotate_v12(key, B, halves, in, mu, u_a, u_b, s, guard, base, n);
-            if (e != hipSuccess) return e;
-        } else if (v6_pair(key, n)) {
+        if (v6_pair(key, n)) {
             const long wgs = (n + 1) / 2;
             // the pair sync's bounded poll hands a ciphertext whose partner never arrives to the
             // guard (bad flag -> exact recomputation): only with guard flags to hand it to

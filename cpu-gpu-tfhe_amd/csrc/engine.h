@@ -27,7 +27,7 @@ struct DeviceKey {
 constexpr int kTw2Words = 2 * 16 * 2 + 2 * 27 * 64 + 2 * 18 * 64;   // uint2 entries
 constexpr int kTw4Words = 2 * 16 + 2 * 27 * 64 + 2 * 16 * 64;
 // double2 entries (blind_rotate_v6.hip build_v6_twiddles)
-constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64 + 21 * 64;   // fft_wave.h table map
+constexpr int kTw6Words = 4 + 4 * 4 * 64 + 8 * 64 + 2 * 64;   // fft_wave.h table map
 
 // x = (0, c) + sa * X + sb * Y   (gate prologue, boot-gates.cu:98-397; Y unused if sb == 0)
 struct BrInput {
@@ -135,16 +135,12 @@ hipError_t launch_bk_to_fft(const int32_t *d_bk_coef, double2 *d_bkf, const doub
 // guard != null: write the rounding-distance flags (Guard) for the guard launch that follows
 hipError_t launch_blind_rotate_v6(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
                                   int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard = nullptr);
-// v12 (four waves per ciphertext, blind_rotate_v12.hip): ciphertexts [base, base + n) of the launch
-hipError_t launch_blind_rotate_v12(const DeviceKey &key, int B, int halves, const BrInput *in, int32_t mu,
-                                   int32_t *u_a, int32_t *u_b, hipStream_t s, const Guard *guard, long base,
-                                   long n);
 hipError_t launch_blind_rotate_v6_rows(const DeviceKey &key, int B, int nrows, const CircRow *rows, const int32_t *wa,
                                        const int32_t *wb, int32_t mu, int32_t *u_a, int32_t *u_b, hipStream_t s,
                                        const Guard *guard = nullptr);
 hipError_t launch_blind_rotate_v6_debug(const DeviceKey &key, int B, int iters, int32_t *acc,
                                         const int32_t *bara, hipStream_t s);
-// which blind-rotation kernel runs: 0 = default (v6 / v12), 4 = exact NTT (tfhe_amd_select_kernel)
+// which blind-rotation kernel runs: 0 = default (v6), 4 = exact NTT (tfhe_amd_select_kernel)
 int br_version();
 // Launch trace: every launcher names the kernel (and variant) it enqueues; a batch entry point of
 // the C ABI collects the names of its launches into its context (tfhe_amd_last_kernels), so a

@@ -24,9 +24,6 @@ constexpr int kTwPost = 1028;
 // post-twist)
 constexpr int kTwSig = 1540;
 constexpr int kTwInvAs = 1604;
-// [1668, 3012) the four-wave kernel's per-lane twiddles (blind_rotate_v12.hip load_tw12): [h][6][64]
-// forward (passes B', C', D': stage a, stage b), then [9][64] inverse
-constexpr int kTw12 = 1668;
 
 __device__ __forceinline__ double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 

@@ -265,8 +265,8 @@ int tfhe_amd_export_lwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_
 int tfhe_amd_export_tlwe_key(const TFheGateBootstrappingSecretKeySet *key, int32_t *out);
 
 /* Select the blind-rotation kernel generation: 0 = default (= 6: fp64 FFT external product,
- * the reference's arithmetic, with the exactness guard above; launches of at most one ciphertext
- * per CU run its four-wave form v12), 4 = the exact 2-prime NTT kernel for every launch.  Returns
+ * the reference's arithmetic, with the exactness guard above), 4 = the exact 2-prime NTT kernel for
+ * every launch.  Returns
  * TFHE_AMD_E_ARG for a generation this build lacks.  Process-wide; results are identical. */
 int tfhe_amd_select_kernel(int br_version);
 

@@ -1,6 +1,8 @@
 """emu_v12.py — numpy emulation of the v12 (four waves per ciphertext) blind-rotation step, layout
 by layout, before any HIP: checks that the half-transform data flow computes the exact negacyclic
-external product and equals v6's transform slot for slot.
+external product and equals v6's transform slot for slot.  (Round 6: v12 was then built from this,
+was Torus32-exact on the GPU first time and measured 2.6 % slower than v6 at B = 1; removed from
+the library, DESIGN.md §5.6, profiles/r06_v12_four_wave_latency_priced.txt.)
 
 v12 splits each 512-point transform at its first Cooley-Tukey stage.  Stage 0 of the merged-twist
 transform (emu_v6.twiddles_v6) maps z_n, z_{n+256} to u + W0 v (slots 0..255, "half 0") and

@@ -101,7 +101,9 @@ def test_register_rotation_equals_negacyclic_rotation(rng):
 
 
 def test_four_wave_half_transforms_emulation():
-    """The four-wave kernel (blind_rotate_v12.hip, scripts/emu_v12.py): stage 0 split into halves,
+    """The four-wave latency design of round 6 (scripts/emu_v12.py; built as blind_rotate_v12.hip, exact
+    on the GPU, measured 2.6 % slower than v6 at B = 1 and removed: DESIGN.md §5.6, profiles/r06_v12_*):
+    stage 0 split into halves,
     four radix-4 passes per half over layouts A' B' C' D', the key read at v6's layout, the DIT
     inverse inside each half with the lane factor folded into pass A', stage 8 across the halves:
     v6's spectrum slot for slot and the exact negacyclic product."""
@@ -110,7 +112,7 @@ def test_four_wave_half_transforms_emulation():
 
 
 def test_four_wave_lds_slot_maps_conflict_free():
-    """The slot maps of blind_rotate_v12.hip's transposes (sAB, sBC, sCD): every 16-B store (8-lane
+    """The slot maps of the four-wave design's transposes (sAB, sBC, sCD): every 16-B store (8-lane
     groups, 128-B rows) and 16-B load (the four 16-lane groups of ds_read_b128, 256-B rows) of every
     transpose they serve hits distinct banks (MI355X_MICROARCH.md §LDS), and each map is one to one
     within its buffer."""

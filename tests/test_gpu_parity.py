@@ -270,36 +270,6 @@ def test_host_batch_slices(ctx, okey, keyset, rng):
     assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b)
 
 
-@pytest.mark.parametrize("gate,B", [("NAND", 256), ("XOR", 1), ("AND", 3), ("MUX", 128), ("NOR", 255)])
-def test_four_wave_kernel_every_output(ctx, okey, keyset, rng, gate, B):
-    """Launches of at most one ciphertext per CU run the four-wave kernel k_blind_rotate_v12
-    (blind_rotate_v12.hip; a MUX of 128 is 256 rotations): every output equals the exact oracle
-    Torus32 for Torus32, with no ciphertext handed to the guard's recomputation."""
-    k = 3 if gate == "MUX" else 2
-    vals = [rng.integers(0, 2, B) for _ in range(k)]
-    cts = [x for v in vals for x in keyset.encrypt(v, rng)]
-    ctx.guard_stats(reset=True)
-    r = ctx.gate_host(gate, *cts)
-    assert any("v12" in x for x in ctx.last_kernels()), ctx.last_kernels()
-    _, redo = ctx.guard_stats(reset=True)
-    w = okey.gate_batch(gate, *cts, nthreads=O.max_threads())
-    assert np.array_equal(r[0], w[0]) and np.array_equal(r[1], w[1])
-    assert redo == 0
-
-
-def test_four_wave_kernel_seams_beside_paired(ctx, okey, keyset, rng):
-    """Above one ciphertext per CU the paired v6 kernel takes over (B = 300 gates: one launch); the
-    same inputs' first 256 through v12 give the same words as through v6p."""
-    B = 300
-    x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
-    (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
-    big = ctx.gate_host("NAND", a_a, a_b, b_a, b_b)
-    assert not any("v12" in k for k in ctx.last_kernels()), ctx.last_kernels()
-    small = ctx.gate_host("NAND", a_a[:256], a_b[:256], b_a[:256], b_b[:256])
-    assert any("v12" in k for k in ctx.last_kernels()), ctx.last_kernels()
-    assert np.array_equal(big[0][:256], small[0]) and np.array_equal(big[1][:256], small[1])
-
-
 def test_host_trace_subprocess(keyset, rng, tmp_path):
     """TFHE_AMD_HOST_TRACE=1 (read once per process): one stderr line per host-pointer batch call with
     its host-side phases (staged, sliced and pinned paths), and the results are unchanged."""
