@@ -30,7 +30,7 @@ for s in "$@"; do
     smoke) c="timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.txt 2>&1" ;;
     bench|bench:*) n="${s#bench}"; n="${n#:}"; n="${n:-default}"
       c="timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_$n.json 2> $O/bench_$n.err" ;;
-    profile) c="timeout -k 10 1500 bash scripts/profile_round.sh $TAG bench > $O/profile.txt 2>&1" ;;
+    profile) c="timeout -k 10 1150 bash scripts/profile_round.sh $TAG bench > $O/profile.txt 2>&1" ;;
     profile_headline) c="timeout -k 10 900 bash scripts/profile_round.sh $TAG headline > $O/profile.txt 2>&1" ;;
     gloo2) c="TFHE_AMD_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 --host-batches none > $O/bench_2ranks.json 2> $O/bench_2ranks.err" ;;
     sweep:*) b="${s#sweep:}"; c="BATCHES='${b//,/ }' timeout -k 10 600 bash scripts/batch_sweep.sh $TAG/sweep > /dev/null 2>&1" ;;
