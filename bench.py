@@ -443,6 +443,8 @@ def circuits_leg(T, torch, ctx, K, rank, world, dist, red_dev, rows5=64, shard5=
                                   "what": "one rank's share of the 8-GPU run, on this GPU"}})
     else:
         lo, hi = matvec.shard_rows(rows5, rank, world)
+        if hi == lo:   # more ranks than rows (world > 64): this rank repeats row 0, so every rank
+            lo, hi = 0, 1   # still joins the leg's barriers and reductions
         rows_run(lo, min(hi, lo + 1), True)                 # schedule tables + warm-up, one row
         t, ok = rows_run(lo, hi, False)
         c5.update({"rows_per_rank": hi - lo, "seconds": t, "bootstraps_per_s": info["bootstraps"] * rows5 / t,
