@@ -144,7 +144,9 @@ int tfhe_amd_keyswitch_batch_host(TfheAmdContext *ctx, int B,
 
 /* Debug/parity entry: run `iters` CMux steps of the blind rotation (i = 0..iters-1,
  * tfhe_MuxRotate_FFT, skipping bara_i == 0 like tfhe_blindRotate_FFT) on B explicit
- * accumulators acc [B][2][1024] in place, with rotations bara [B][iters]. */
+ * accumulators acc [B][2][1024] in place, with rotations bara [B][iters].  The raw steps of the
+ * selected kernel generation, WITHOUT the exactness guard (the fp64 kernel's roundings are not
+ * checked): a kernel-test entry.  The exact L1 function is tfhe_blindRotate_FFT (tfhe.h). */
 int tfhe_amd_blind_rotate_dev(TfheAmdContext *ctx, int B, int iters, int32_t *acc,
                               const int32_t *bara, void *stream);
 /* tGswFFTExternMulToTLwe (tgsw_functions.h:70, tgsw-fft-operations.cu:124-264) on B accumulators:
