@@ -53,3 +53,21 @@ def test_bench_line_fields():
         assert k in cb, k
     assert cb["kind"] in ("port", "reference") and cb["value"] > 0
     assert d["truth_table_ok"] is True and d["parity"]["mismatches"] == 0
+
+
+@pytest.mark.gpu
+def test_bench_circuits_leg_small(keyset, ctx):
+    """bench.py's `circuits` leg (BASELINE configs 3-5) at a reduced matrix: every entry carries
+    seconds, bootstraps/s, depth and a decrypted-correct flag, and every flag is True."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    import bench
+    import tfhe_amd as T
+    out = bench.circuits_leg(T, torch, ctx, keyset, 0, 1, dist, "cpu", rows5=4, shard5=2)
+    for name in ("config3_add32", "config4_mul16_b256", "config5_matvec64"):
+        e = out[name]
+        assert e["correct"] is True, (name, e)
+        assert e["seconds"] > 0 and e["bootstraps_per_s"] > 0 and e["depth"] > 0, (name, e)
+    assert out["config3_add32"]["depth"] == 32 and out["config3_add32"]["bootstraps_per_instance"] == 64
+    assert out["config5_matvec64"]["rows_per_rank"] == 4 and out["config5_matvec64"]["shard_of_8"]["rows"] == 2
