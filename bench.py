@@ -413,6 +413,10 @@ def circuits_leg(T, torch, ctx, K, rank, world, dist, red_dev, rows5=64, shard5=
     out = {}
     out["config3_add32"] = binop("add32", lambda C, a, b: (lambda s: s[0] + [s[1]])(C.add(a, b)), 32, 1, 5,
                                  lambda x, y: x + y, "32-bit ripple-carry add, one instance per rank")
+    out["config3_add32_prefix"] = binop("add32p", lambda C, a, b: (lambda s: s[0] + [s[1]])(C.add_prefix(a, b)), 32, 1,
+                                        5, lambda x, y: x + y,
+                                        "the same 32-bit addition as a parallel-prefix circuit (fewer levels, "
+                                        "more gates per level): what a caller gains by not following the ripple")
     out["config4_mul16_b256"] = binop("mul16", lambda C, a, b: C.mul(a, b), 16, 256, 2, lambda x, y: x * y,
                                       "16 x 16 -> 32-bit multiply (Dadda tree), 256 instances per rank")
     # config 5: the same matrix and vector on every rank, this rank's rows

@@ -65,7 +65,7 @@ def test_bench_circuits_leg_small(keyset, ctx):
     import bench
     import tfhe_amd as T
     out = bench.circuits_leg(T, torch, ctx, keyset, 0, 1, dist, "cpu", rows5=4, shard5=2)
-    for name in ("config3_add32", "config4_mul16_b256", "config5_matvec64"):
+    for name in ("config3_add32", "config3_add32_prefix", "config4_mul16_b256", "config5_matvec64"):
         e = out[name]
         assert e["correct"] is True, (name, e)
         assert e["seconds"] > 0 and e["bootstraps_per_s"] > 0 and e["depth"] > 0, (name, e)
