@@ -166,9 +166,10 @@ def test_paired_workgroups_bit_exact(ctx, okey, keyset, rng):
     x, y = rng.integers(0, 2, B), rng.integers(0, 2, B)
     (a_a, a_b), (b_a, b_b) = keyset.encrypt(x, rng), keyset.encrypt(y, rng)
     r_a, r_b = ctx.gate_host("AND", a_a, a_b, b_a, b_b)
-    assert any("v6p(paired+reg-rotation+pair-sync)" in k for k in ctx.last_kernels()), ctx.last_kernels()
+    kern = ctx.last_kernels()
     o_a, o_b = okey.gate_batch("AND", a_a, a_b, b_a, b_b)
-    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)
+    assert np.array_equal(r_a, o_a) and np.array_equal(r_b, o_b)   # parity first, then which kernel
+    assert any("v6p(paired+reg-rotation+pair-sync)" in k for k in kern), kern
     B = 199                                   # MUX: 398 rotations; rotations 198 | 199 share a workgroup
     s, x, y = (rng.integers(0, 2, B) for _ in range(3))
     (sa, sb), (xa, xb), (ya, yb) = (keyset.encrypt(v, rng) for v in (s, x, y))
@@ -489,9 +490,10 @@ rng = np.random.default_rng(6)
 x, y = rng.integers(0, 2, 301), rng.integers(0, 2, 301)
 (a_a, a_b), (b_a, b_b) = K.encrypt(x, rng), K.encrypt(y, rng)
 r = c.gate_host("NAND", a_a, a_b, b_a, b_b)
-assert any("v6p(paired+reg-rotation)" in k for k in c.last_kernels()), c.last_kernels()
+kern = c.last_kernels()
 w = o.gate_batch("NAND", a_a, a_b, b_a, b_b)
-assert np.array_equal(r[0], w[0]) and np.array_equal(r[1], w[1])
+assert np.array_equal(r[0], w[0]) and np.array_equal(r[1], w[1])   # parity first, then which kernel
+assert any("v6p(paired+reg-rotation)" in k for k in kern), kern
 s, x, y = (rng.integers(0, 2, 199) for _ in range(3))
 (sa, sb), (xa, xb), (ya, yb) = (K.encrypt(v, rng) for v in (s, x, y))
 r = c.gate_host("MUX", sa, sb, xa, xb, ya, yb); w = o.gate_batch("MUX", sa, sb, xa, xb, ya, yb)
@@ -534,7 +536,7 @@ def test_mixed_gate_batch_bit_exact(ctx, okey, keyset, rng):
         xa, xb, xc = (rng.integers(0, 2, B) for _ in range(3))
         (aa, ab), (ba, bb), (ca, cb) = (keyset.encrypt(v, rng) for v in (xa, xb, xc))
         r_a, r_b = ctx.gate_mixed_host(gates, aa, ab, ba, bb, ca, cb)
-        assert "k_blind_rotate_v6_rows" in ",".join(ctx.last_kernels())
+        kern = ",".join(ctx.last_kernels())
         g = np.array(gates)
         for name in names:
             idx = np.flatnonzero(g == name)
@@ -545,3 +547,4 @@ def test_mixed_gate_batch_bit_exact(ctx, okey, keyset, rng):
             assert np.array_equal(r_a[idx], o_a) and np.array_equal(r_b[idx], o_b), (B, name)
             want = truth[name](xa[idx], xb[idx], xc[idx])
             assert np.array_equal(keyset.decrypt(r_a[idx], r_b[idx]), want), (B, name)
+        assert "k_blind_rotate_v6_rows" in kern, kern   # parity first, then which kernel
