@@ -185,50 +185,54 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
         uint32_t V[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) V[r] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)acc[r]);
-        // RSW (the one-ciphertext-per-workgroup kernels of launches above 2 ciphertexts per CU,
-        // i.e. the throughput launches): one of 32 static register permutations chosen by a scalar branch
-        // tree on q — 16 moves / negations instead of up to 5 conditional stages of 16 (B = 1 024
-        // / 4 096 -0.5 / -0.35 %; at B = 512, one wave per SIMD, the branch tree on the critical
-        // path costs +1 %, so the paired kernel keeps the stages: profiles/r03_rswitch_ab.txt)
-        if constexpr (RSW) {
-            uint32_t O[16];
-            switch (q) {
-#define V6_ROT_CASE(Q)                                                                            \
-    case Q: {                                                                                     \
-        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                          \
-            const int k = r - (Q);                                                                \
-            O[r] = k >= 0 ? V[k] : (k >= -16 ? 0u - V[k + 16] : V[k + 32]);                       \
-        }                                                                                         \
-    } break;
-                V6_ROT_CASE(0) V6_ROT_CASE(1) V6_ROT_CASE(2) V6_ROT_CASE(3) V6_ROT_CASE(4) V6_ROT_CASE(5)
-                V6_ROT_CASE(6) V6_ROT_CASE(7) V6_ROT_CASE(8) V6_ROT_CASE(9) V6_ROT_CASE(10) V6_ROT_CASE(11)
-                V6_ROT_CASE(12) V6_ROT_CASE(13) V6_ROT_CASE(14) V6_ROT_CASE(15) V6_ROT_CASE(16) V6_ROT_CASE(17)
-                V6_ROT_CASE(18) V6_ROT_CASE(19) V6_ROT_CASE(20) V6_ROT_CASE(21) V6_ROT_CASE(22) V6_ROT_CASE(23)
-                V6_ROT_CASE(24) V6_ROT_CASE(25) V6_ROT_CASE(26) V6_ROT_CASE(27) V6_ROT_CASE(28) V6_ROT_CASE(29)
-                V6_ROT_CASE(30)
-                default: V6_ROT_CASE(31)
-#undef V6_ROT_CASE
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) V[r] = O[r];
-        }
-        if (!RSW && (q & 16)) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) V[r] = 0u - V[r];
-        }
-#pragma unroll
-        for (int K = 8; K >= 1; K >>= 1) {
-            if (!RSW && (q & K)) {
-                uint32_t t[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t[r] = r >= K ? V[r - K] : 0u - V[r + 16 - K];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) V[r] = t[r];
-            }
-        }
         const bool lo = L < s;
+        if constexpr (RSW) {
+            // RSW (the one-ciphertext-per-workgroup kernels of launches above 2 ciphertexts per
+            // CU, i.e. the throughput launches): one of 32 static register permutations chosen by a
+            // scalar branch tree on q, with the lane select L < s folded into each case, so every
+            // case writes the 16 digit sources straight from V: 16 selects plus its negations
+            // instead of up to 5 conditional stages of 16 (B = 1 024 / 4 096 -0.5 / -0.35 %
+            // against the stages, profiles/r03_rswitch_ab.txt; the fold another -1.2 / -1.1 %,
+            // profiles/r06m_rswitch_select_ab.txt).  At B = 512, one wave per SIMD, the branch tree
+            // on the critical path costs +1 %, so the paired kernel keeps the stages.
+            uint32_t O[16];
+            // register k of the negacyclic ring of 32 (k in [-32, 16)): V, or its negation below 0
+            auto ring = [&](int k) -> uint32_t { return k >= 0 ? V[k] : (k >= -16 ? 0u - V[k + 16] : V[k + 32]); };
+            switch (q) {
+#define V6_SEL_CASE(Q)                                                                            \
+    case Q: {                                                                                     \
+        _Pragma("unroll") for (int r = 0; r < 16; ++r)                                            \
+            O[r] = lo ? (r ? ring(r - 1 - (Q)) : 0u - ring(15 - (Q))) : ring(r - (Q));            \
+    } break;
+                V6_SEL_CASE(0) V6_SEL_CASE(1) V6_SEL_CASE(2) V6_SEL_CASE(3) V6_SEL_CASE(4) V6_SEL_CASE(5)
+                V6_SEL_CASE(6) V6_SEL_CASE(7) V6_SEL_CASE(8) V6_SEL_CASE(9) V6_SEL_CASE(10) V6_SEL_CASE(11)
+                V6_SEL_CASE(12) V6_SEL_CASE(13) V6_SEL_CASE(14) V6_SEL_CASE(15) V6_SEL_CASE(16) V6_SEL_CASE(17)
+                V6_SEL_CASE(18) V6_SEL_CASE(19) V6_SEL_CASE(20) V6_SEL_CASE(21) V6_SEL_CASE(22) V6_SEL_CASE(23)
+                V6_SEL_CASE(24) V6_SEL_CASE(25) V6_SEL_CASE(26) V6_SEL_CASE(27) V6_SEL_CASE(28) V6_SEL_CASE(29)
+                V6_SEL_CASE(30)
+                default: V6_SEL_CASE(31)
+#undef V6_SEL_CASE
+            }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) digits(r, lo ? (r ? V[r - 1] : 0u - V[15]) : V[r]);
+            for (int r = 0; r < 16; ++r) digits(r, O[r]);
+        } else {
+            if (q & 16) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) V[r] = 0u - V[r];
+            }
+#pragma unroll
+            for (int K = 8; K >= 1; K >>= 1) {
+                if (q & K) {
+                    uint32_t t[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) t[r] = r >= K ? V[r - K] : 0u - V[r + 16 - K];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) V[r] = t[r];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) digits(r, lo ? (r ? V[r - 1] : 0u - V[15]) : V[r]);
+        }
     } else {
         write_ext(E, acc, L);
         wave_sync();
@@ -423,7 +427,11 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
+#ifdef TFHE_AMD_V6P_RSW
+        cmux_v6<WAVES, RREG, RREG, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
+#else
         cmux_v6<WAVES, RREG, RREG && C == 1, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
+#endif
                                                  seq V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
