@@ -194,7 +194,8 @@ __device__ __forceinline__ void cmux_v6(V6Ct &sh, const double2 *shtw, const V6A
             // instead of up to 5 conditional stages of 16 (B = 1 024 / 4 096 -0.5 / -0.35 %
             // against the stages, profiles/r03_rswitch_ab.txt; the fold another -1.2 / -1.1 %,
             // profiles/r06m_rswitch_select_ab.txt).  At B = 512, one wave per SIMD, the branch tree
-            // on the critical path costs +1 %, so the paired kernel keeps the stages.
+            // on the critical path cost +1 %, and with the fold it is neutral (profiles/r06n_*),
+            // so the paired kernel keeps the stages.
             uint32_t O[16];
             // register k of the negacyclic ring of 32 (k in [-32, 16)): V, or its negation below 0
             auto ring = [&](int k) -> uint32_t { return k >= 0 ? V[k] : (k >= -16 ? 0u - V[k + 16] : V[k + 32]); };
@@ -427,11 +428,7 @@ __device__ __forceinline__ void br_v6_body(V6Ct &sh, double2 *shtw, const V6Args
                 set_prio_level(2u * (unsigned)(blockIdx.x / g.cus) + ((unsigned)i >> g.prio_shift));
         }
         if (C == 1 && a == 0) continue;  // X^0 - 1 = 0: identity CMux (:705)
-#ifdef TFHE_AMD_V6P_RSW
-        cmux_v6<WAVES, RREG, RREG, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
-#else
         cmux_v6<WAVES, RREG, RREG && C == 1, PS>(sh, shtw, g, tA, i, a, w, own, L, acc, mx, hlo, hhi, bad,
-#endif
                                                  seq V6_STAMPS_ARG);
     }
     if (g.flags && live) {   // exactness guard: this wave's largest rounding distance (high word)
