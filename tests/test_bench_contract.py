@@ -23,6 +23,20 @@ def test_bench_help_runs_without_gpu():
     assert r.returncode == 0 and "--steps" in r.stdout and "--warmup" in r.stdout
 
 
+def test_committed_pmc_summary_is_the_headlines():
+    """bench.py's `roofline.traffic` comes from profiles/pmc_summary.json only when that summary is
+    the headline's (this library's engine string, B = 1 024, the throughput kernel): a summary of
+    another batch (a B = 1 counter pass once overwrote it) would silently null the field."""
+    sys.path.insert(0, REPO)
+    import bench
+    import tfhe_amd as T
+    s = json.load(open(os.path.join(REPO, "profiles", "pmc_summary.json")))
+    assert s["batch"] == 1024 and s["engine"] == T.version(), (s["batch"], s["engine"])
+    assert "k_blind_rotate_v6<2, true>" in s["kernels"]["blind_rotate"]["kernel"]
+    traffic, src = bench.pmc_traffic(T.version(), 1024)
+    assert traffic and traffic > 0 and src
+
+
 @pytest.mark.gpu
 def test_bench_line_fields():
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "2",
