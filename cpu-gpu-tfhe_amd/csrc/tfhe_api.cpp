@@ -583,7 +583,7 @@ struct Tier1Req {
 // sleep on their own request: a finished batch's leader does its callers' bookkeeping and wakes
 // exactly them, and a freed lane wakes the oldest pending caller to lead (no wake-up of every
 // thread in the call per batch, which serialised 64 threads on the queue lock).
-// The window adapts to the callers: it starts at TFHE_AMD_TIER1_WINDOW_US (default 200 us),
+// The window adapts to the callers: it starts at the floor below (200 us),
 // follows 4x the average wait that ended with every expected thread enqueued (+ 20 us), and
 // shrinks by a quarter after a wait that timed out (callers busy elsewhere), within [200, 1000] us.
 constexpr int kQueueLanes = 2;
@@ -943,11 +943,6 @@ static bool coalesce_enabled() {
     }();
     return on;
 }
-// a free lane merges the next batch into a running one below one ciphertext per CU (without
-// merging: 20.3-25.8 k/s against 26.3-27.4, profiles/r04i_*)
-static bool merge_enabled() { return true; }
-// the leader's shortest straggler window for the threads inside a call
-static int coalesce_window_us() { return 200; }
 
 static double *ks_variance_table(const TFheGateBootstrappingCloudKeySet *bk) {
     // the KSK row variances on the device, once per key: each slice's current_variance is summed by
@@ -1101,7 +1096,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
     req.b = b;
     req.c = c;
     std::unique_lock<std::mutex> lk(q.mu);
-    if (q.window_us < 0) q.window_us = coalesce_window_us();
+    if (q.window_us < 0) q.window_us = kWindowFloorUs;
     q.inside += 1;
     if (q.returning > 0) q.returning -= 1;
     q.pending.push_back(&req);
@@ -1142,7 +1137,7 @@ static void gate1(int gate, LweSample *r, const LweSample *a, const LweSample *b
         // hold at most one ciphertext per CU, a second launch beside it only shares its CUs (two
         // latency-class launches of 31 run 2.15 ms each; one of 62 about 1.8), so wait for that batch
         // and take its callers' next gates too
-        if (merge_enabled() && q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= q.merge_limit) {
+        if (q.in_flight > 0 && (int)q.pending.size() + q.in_flight <= q.merge_limit) {
             const auto t0 = std::chrono::steady_clock::now();
             q.arrive_cv.wait(lk, [&] { return q.in_flight == 0; });
             bms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

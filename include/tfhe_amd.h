@@ -234,8 +234,8 @@ int tfhe_amd_tier1_lane_count(const TFheGateBootstrappingCloudKeySet *bk);
 /* Concurrent Tier-1 gate calls on one key are coalesced: a calling thread enqueues its gate; a
  * waiting thread that finds one of the queue's two lanes free becomes the leader of the next
  * batch: it waits until every thread inside a gate call and not in a running batch has enqueued
- * (an adaptive window: TFHE_AMD_TIER1_WINDOW_US, default 200 us, at first, then 4x the observed
- * wait, within 200 - 1000 us), takes every pending gate and runs them on its lane — one gate kind
+ * (an adaptive window: 200 us at first, then 4x the observed wait + 20 us, within 200 - 1000 us),
+ * takes every pending gate and runs them on its lane — one gate kind
  * as one gate batch, several kinds as one mixed launch (one blind rotation + one key switch) per
  * 512 gates — while later calls queue for the next batch, which the other lane can stage and
  * launch while this one is still running (a lone thread runs its gate at once, B = 1).  Results,
