@@ -697,6 +697,11 @@ static int v6_prio_policy(const DeviceKey &key, long wgs, bool paired = false) {
     return wgs > 4L * v6_cus(key) ? 1 : 5;
 }
 
+// policy 5's steps per priority level = 2^kV6PrioShift (variant builds: -DTFHE_AMD_V6_PRIO_SHIFT=n)
+#ifndef TFHE_AMD_V6_PRIO_SHIFT
+#define TFHE_AMD_V6_PRIO_SHIFT 3
+#endif
+constexpr int kV6PrioShift = TFHE_AMD_V6_PRIO_SHIFT;
 static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullptr, bool paired = false) {
     V6Args g;
     g.bk = key.bk_fft;
@@ -704,7 +709,7 @@ static V6Args v6_args(const DeviceKey &key, long wgs, const Guard *guard = nullp
     g.stats = guard ? guard->stats : nullptr;
     g.tw = key.tw6;
     g.prio = wgs > 0 ? v6_prio_policy(key, wgs, paired) : 0;
-    g.prio_shift = 3;
+    g.prio_shift = kV6PrioShift;
     g.cus = v6_cus(key);
     return g;
 }
