@@ -89,15 +89,36 @@ def _rotate_rreg(acc, a):
     return out.reshape(-1)                               # index r * 64 + L = coefficient L + 64 r
 
 
+def _rotate_rsw_fold(acc, a):
+    """numpy restatement of the throughput kernels' form (cmux_v6 RSW, round 6): the permutation
+    case q writes each digit source straight from the bpermuted registers V through ring(k)
+    (k in [-32, 16): V[k], its negation for k < 0, V[k + 32] below -16), lanes L < s taking
+    ring(r - 1 - q) and, for r = 0, -ring(15 - q)."""
+    aa = a & 2047
+    s, q = aa & 63, aa >> 6
+    reg = acc.reshape(16, 64).astype(np.int64)
+    V = reg[:, (np.arange(64) - s) % 64]
+
+    def ring(k):
+        return V[k] if k >= 0 else (-V[k + 16] if k >= -16 else V[k + 32])
+    lo = np.arange(64) < s
+    out = np.stack([np.where(lo, ring(r - 1 - q) if r else -ring(15 - q), ring(r - q)) for r in range(16)])
+    return (out & 0xFFFFFFFF).astype(np.uint32).reshape(-1)
+
+
 def test_register_rotation_equals_negacyclic_rotation(rng):
     """The register rotation gives X^a ACC (negacyclic, mod 2^32) for every a the kernel can see,
-    including 0, multiples of 64 and the wrap through 1024 and 2048."""
+    including 0, multiples of 64 and the wrap through 1024 and 2048 — the staged form (paired
+    kernel) and the throughput kernels' permutation switch with the lane select folded in."""
     acc = rng.integers(0, 2**32, 1024, dtype=np.uint64).astype(np.uint32)
     ext = np.concatenate([acc, (0 - acc.astype(np.int64)).astype(np.uint32)])    # E[k], k < 2N
     for a in list(range(0, 130)) + [511, 512, 513, 960, 1023, 1024, 1025, 1087, 1088, 1984, 2047, 2048] + \
             list(rng.integers(0, 2049, 64)):
         want = ext[(np.arange(1024) - a) % 2048]        # (X^a ACC)[j] = E[(j - a) mod 2N]
         assert np.array_equal(_rotate_rreg(acc, int(a)), want), a
+    for a in range(2049):                                # every case of the permutation switch
+        want = ext[(np.arange(1024) - a) % 2048]
+        assert np.array_equal(_rotate_rsw_fold(acc, a), want), a
 
 
 def test_four_wave_half_transforms_emulation():
