@@ -213,7 +213,7 @@ __device__ __forceinline__ bool guard_skip(const V4Guard &gd, size_t slot) {
 // over the total ciphertexts: one per workgroup normally; in guard mode a small grid scans the
 // flags (almost always all clear) instead of dispatching one workgroup per ciphertext.
 // MINW: waves per SIMD the register budget is cut for — 2 for the exact throughput kernel
-// (TFHE_AMD_BR=4: 256 VGPRs, 27 spilled), 1 for the guard launch (284 VGPRs, no scratch: a
+// (tfhe_amd_select_kernel(4): 256 VGPRs, 27 spilled), 1 for the guard launch (284 VGPRs, no scratch: a
 // kernel with a private segment costs ~12 us more per dispatch even when every workgroup exits
 // at once)
 template <int MINW>
