@@ -62,6 +62,8 @@ def test_bench_line_fields():
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     assert abs(rf["achieved"] - rf["flops_per_launch"] / (rf["kernel_ms"] / 1e3) / 1e12) / rf["achieved"] < 1e-6
     assert 0 < rf["kernel_ms"] < d["ms_per_step"]
+    # the committed PMC summary is the headline's (test_committed_pmc_summary_is_the_headlines)
+    assert rf["traffic"] and rf["traffic"] > 0 and rf["hbm"]["traffic_source"]
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
